@@ -1,0 +1,182 @@
+/*
+ * siren_hip.h -- C-ABI of libsiren_hip.so, the MI355X (gfx950) SIREN audio-fitting path.
+ *
+ * The reference (senyuanfan/inr-for-audio) is pure PyTorch and has no FFI; each entry point
+ * below replaces the torch eager work behind one reference interface, cited as file:line
+ * into the reference tree.  Conventions:
+ *   - every pointer is a DEVICE pointer owned by the caller (torch allocates; the library
+ *     never allocates, frees or synchronises the host);
+ *   - bf16 tensors are passed as uint16_t*, row-major; fp32 weights use the nn.Linear
+ *     layout [out_features][in_features];
+ *   - `stream` is a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ *   - every function returns 0 on success, or a non-zero siren_status / hipError_t code
+ *     (see siren_status_string), and never aborts the process.
+ */
+#ifndef SIREN_HIP_H
+#define SIREN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIREN_ABI_VERSION 1
+#define SIREN_MAX_INNER 16  /* max hidden SineLayers (num_sine) */
+#define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
+
+enum siren_status {
+  SIREN_OK = 0,
+  SIREN_ERR_SHAPE = 1001,   /* unsupported / inconsistent shape            */
+  SIREN_ERR_NULL = 1002,    /* required pointer missing                    */
+  SIREN_ERR_CONFIG = 1003   /* unsupported configuration (e.g. in_dim > 2) */
+};
+
+int siren_abi_version(void);
+const char* siren_status_string(int status);
+
+/* ---- device-resident optimizer state: torch.optim.Adam + ReduceLROnPlateau ------------
+ * run.py:116-117 (Adam(lr), ReduceLROnPlateau(mode='min', factor=0.8, patience=200,
+ * min_lr=min_learning_rate)).  Layout shared with the Python mirror. */
+typedef struct siren_opt_state {
+  double lr, best, step;
+  int32_t num_bad, last_epoch;
+  double min_lr, factor, threshold, eps_lr;
+  int32_t patience, pad0;
+  double beta1, beta2, eps;
+} siren_opt_state;
+
+/* ---- one SIREN L x H network (SirenWithSnakeTanh, sine-only; models.py:306-394) --------
+ * net.0 = SineLayer(in, H, is_first, omega0); net.1..net.L = SineLayer(H, H, omega);
+ * net.{L+1} = Linear(H, 1).  Inner layer i (0-based) is net.{i+1}. */
+typedef struct siren_net {
+  int32_t in_dim, hidden, n_inner, pad0;
+  float omega0, omega;
+  const float* W0;                          /* [H][in]  fp32 */
+  const float* b0;                          /* [H]           */
+  const float* b[SIREN_MAX_INNER];          /* [H]           */
+  const uint16_t* Wb[SIREN_MAX_INNER];      /* [H][H] bf16 shadow of W_i   */
+  const uint16_t* WTb[SIREN_MAX_INNER];     /* [H][H] bf16 shadow of W_i^T */
+  const float* w_head;                      /* [H] (net.{L+1}.weight[0])   */
+  const float* b_head;                      /* [1]                          */
+} siren_net;
+
+/* gradient destinations (fp32, accumulated into: zero them, or set zero_grads) */
+typedef struct siren_grads {
+  float* W0; float* b0;
+  float* W[SIREN_MAX_INNER]; float* b[SIREN_MAX_INNER];
+  float* w_head; float* b_head;
+  float* sse;                               /* [1] sum of squared errors of valid rows */
+  float* flat; int64_t flat_len;            /* if flat != NULL and zero_grads: memset   */
+} siren_grads;
+
+/* per-micro-batch activations and workspace; sizes from siren_workspace_floats() */
+typedef struct siren_batch {
+  int32_t rows;          /* padded rows, multiple of SIREN_ROW_TILE          */
+  int32_t n_valid;       /* valid rows (<= rows)                             */
+  double n_total;        /* global coordinate count: MSE mean denominator    */
+  int32_t splits;        /* split-K slices of the weight-gradient GEMM       */
+  int32_t zero_grads;    /* 1: zero `grads.flat` before accumulating         */
+  const float* coords;   /* [rows][in]  */
+  const float* target;   /* [rows]      */
+  uint16_t* Y[SIREN_MAX_INNER + 1];  /* Y[0..L] bf16 [rows][H]: layer outputs sin(.)  */
+  uint16_t* C[SIREN_MAX_INNER + 1];  /* C[1..L] bf16 [rows][H]: cos(.) of inner layers */
+  uint16_t* dZ[2];       /* bf16 [rows][H] ping-pong pre-activation gradients   */
+  float* out;            /* [rows] model output                                 */
+  float* g;              /* [rows] dLoss/dout                                   */
+  float* head_part;      /* [H/128][rows]                                       */
+  float* sse_part;       /* [rows/256]                                          */
+  float* gsum_part;      /* [rows/256]                                          */
+  float* col_part;       /* [rows/128][1+in][H]                                 */
+  float* col_part2;      /* [rows/128][H]                                       */
+  float* red_tmp;        /* [64][H]                                             */
+  float* slab;           /* [splits][H][H]                                      */
+} siren_batch;
+
+/* Workspace sizing helpers (element counts). */
+int32_t siren_default_splits(int32_t rows, int32_t hidden);
+int64_t siren_slab_floats(int32_t hidden, int32_t splits);
+
+/* ---- fused path ---------------------------------------------------------------------
+ * siren_forward:     run.py:158 / :255  model(model_input) -> batch.out (inference only).
+ * siren_train_step:  run.py:158-185     forward + MSELoss + loss.backward() for one
+ *                    micro-batch; gradients ACCUMULATE into `grads` (global-N scaling).
+ * siren_apply_update:run.py:186-187     optimizer.step() + scheduler.step(loss), then the
+ *                    bf16 weight shadows are refreshed.  (`params`, `grads_flat`, `exp_avg`,
+ *                    `exp_avg_sq` are the flat fp32 vectors of length n_params.)          */
+int siren_forward(const siren_net* net, siren_batch* batch, void* stream);
+int siren_train_step(const siren_net* net, const siren_grads* grads, siren_batch* batch,
+                     void* stream);
+/* loss.backward() through the network for an arbitrary upstream gradient: batch->g holds
+ * dLoss/dout (zero on pad rows) and batch->Y/C the activations of a prior siren_forward. */
+int siren_backward(const siren_net* net, const siren_grads* grads, siren_batch* batch,
+                   void* stream);
+int siren_apply_update(const siren_net* net, float* params, const float* grads_flat,
+                       float* exp_avg, float* exp_avg_sq, int64_t n_params,
+                       float* const* W_fp32 /* [n_inner] views into params */,
+                       uint16_t* const* Wb, uint16_t* const* WTb,
+                       siren_opt_state* state, const float* sse, double n_total,
+                       float* loss_hist, double* lr_hist, int64_t hist_cap, void* stream);
+
+/* ---- individual kernels (parity tests call these one by one) ------------------------ */
+/* utils.py:99-109 get_coord: torch.linspace(-1,1,n_total) at [offset, offset+rows) */
+int siren_coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, void* stream);
+/* models.py:114-115 first SineLayer: Y0 = sin(omega0*(t W0^T + b0)) -> bf16 */
+int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float* b0, float omega0,
+                    int32_t rows, int32_t hidden, uint16_t* Y0, void* stream);
+/* models.py:114-115 hidden SineLayer: Y = sin(omega(X W^T + b)), C = cos(.); optional head
+ * partial dot (models.py:374-381) when head_w != NULL */
+int siren_inner_fwd(const uint16_t* X, const uint16_t* Wb, const float* b, float omega, int32_t rows,
+                    int32_t hidden, uint16_t* Y, uint16_t* C, const float* head_w, float* head_part,
+                    void* stream);
+/* run.py:125,168 MSELoss + final Linear bias: out, g = 2(out-y)/n_total, partial sums */
+int siren_head_loss(const float* head_part, int32_t nparts, int32_t rows, const float* b_head,
+                    const float* y, int32_t n_valid, double n_total, float* out, float* g,
+                    float* sse_part, float* gsum_part, void* stream);
+/* autograd of Linear(H,1) + last sin: dZ_L, db_L partials, dw_head partials */
+int siren_head_bwd(const uint16_t* C, const uint16_t* Y, const float* g, const float* w_head,
+                   float omega, int32_t rows, int32_t hidden, uint16_t* dZ, float* db_part,
+                   float* dwh_part, void* stream);
+/* autograd addmm dX + sin/omega backward of the layer below: dZprev = omega*cos*(dZ W) */
+int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTb, const uint16_t* Cprev, float omega_prev,
+                       int32_t rows, int32_t hidden, uint16_t* dZprev, float* db_part, void* stream);
+/* same into the fp32 first layer: partials [rows/128][1+in][H] of dZ0 and dZ0*t_j */
+int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTb1, const float* t, int32_t in_dim,
+                       const float* W0, const float* b0, float omega0, int32_t rows, int32_t hidden,
+                       float* part, void* stream);
+/* autograd addmm dW: slab[s] = partial dZ^T Y over coordinate slice s */
+int siren_inner_bwd_dw(const uint16_t* Y, const uint16_t* dZ, int32_t rows, int32_t hidden,
+                       int32_t splits, float* slab, void* stream);
+int siren_dw_reduce(const float* slab, int32_t splits, int32_t hidden, float* grad, int32_t accumulate,
+                    void* stream);
+int siren_col_reduce(const float* part, int64_t row_stride, int32_t nrows, int32_t ncols, float* out,
+                     int32_t out_stride, int32_t accumulate, float* tmp, void* stream);
+/* torch.optim.Adam step over a flat fp32 vector (run.py:186) */
+int siren_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                    const siren_opt_state* state, void* stream);
+/* ReduceLROnPlateau.step(loss) (run.py:187); also increments state->step */
+int siren_plateau_step(siren_opt_state* state, const float* sse, double n_total, float* loss_hist,
+                       double* lr_hist, int64_t hist_cap, void* stream);
+/* bf16 shadows W and W^T of a fp32 [H_out][H_in] weight */
+int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wb, uint16_t* WTb,
+                      void* stream);
+
+/* ---- per-launch HIP-event profiling of the fused path (bench.py) --------------------
+ * siren_profile_enable(n) creates 2n hipEvents; while enabled every launch made by
+ * siren_train_step / siren_backward / siren_forward / siren_apply_update is bracketed
+ * by events on its stream (eager launches only; not meant for graph capture).
+ * siren_profile_read sums the elapsed time of all records of one kind (synchronises). */
+enum siren_prof_kind {
+  SIREN_PROF_FIRST_FWD = 0, SIREN_PROF_INNER_FWD = 1, SIREN_PROF_HEAD = 2, SIREN_PROF_BWD_DW = 3,
+  SIREN_PROF_BWD_DX = 4, SIREN_PROF_BWD_DX0 = 5, SIREN_PROF_REDUCE = 6, SIREN_PROF_UPDATE = 7,
+  SIREN_PROF_NKINDS = 8
+};
+int siren_profile_enable(int32_t max_records);
+int siren_profile_reset(void);
+int siren_profile_read(int32_t kind, double* total_ms, int64_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIREN_HIP_H */

@@ -1,0 +1,157 @@
+"""ctypes binding of libsiren_hip.so (the C-ABI declared in include/siren_hip.h).
+
+This is the only place Python touches the native library.  There is deliberately no
+fallback: if the shared object is missing or was built for another ABI, importing the
+compute path raises, so a GPU run can never silently degrade to eager PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  -- load torch's HIP runtime first so the library binds to it
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
+ABI_VERSION = 1
+MAX_INNER = 16
+ROW_TILE = 128
+
+_p = ctypes.c_void_p
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+
+
+class SirenOptState(ctypes.Structure):
+    """siren_opt_state: Adam step + ReduceLROnPlateau state (run.py:116-117)."""
+    _fields_ = [
+        ("lr", ctypes.c_double), ("best", ctypes.c_double), ("step", ctypes.c_double),
+        ("num_bad", _i32), ("last_epoch", _i32),
+        ("min_lr", ctypes.c_double), ("factor", ctypes.c_double),
+        ("threshold", ctypes.c_double), ("eps_lr", ctypes.c_double),
+        ("patience", _i32), ("pad0", _i32),
+        ("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
+    ]
+
+
+class SirenNet(ctypes.Structure):
+    _fields_ = [
+        ("in_dim", _i32), ("hidden", _i32), ("n_inner", _i32), ("pad0", _i32),
+        ("omega0", ctypes.c_float), ("omega", ctypes.c_float),
+        ("W0", _p), ("b0", _p),
+        ("b", _p * MAX_INNER), ("Wb", _p * MAX_INNER), ("WTb", _p * MAX_INNER),
+        ("w_head", _p), ("b_head", _p),
+    ]
+
+
+class SirenGrads(ctypes.Structure):
+    _fields_ = [
+        ("W0", _p), ("b0", _p),
+        ("W", _p * MAX_INNER), ("b", _p * MAX_INNER),
+        ("w_head", _p), ("b_head", _p), ("sse", _p),
+        ("flat", _p), ("flat_len", _i64),
+    ]
+
+
+class SirenBatch(ctypes.Structure):
+    _fields_ = [
+        ("rows", _i32), ("n_valid", _i32), ("n_total", ctypes.c_double),
+        ("splits", _i32), ("zero_grads", _i32),
+        ("coords", _p), ("target", _p),
+        ("Y", _p * (MAX_INNER + 1)), ("C", _p * (MAX_INNER + 1)), ("dZ", _p * 2),
+        ("out", _p), ("g", _p), ("head_part", _p), ("sse_part", _p), ("gsum_part", _p),
+        ("col_part", _p), ("col_part2", _p), ("red_tmp", _p), ("slab", _p),
+    ]
+
+
+# name -> (restype, argtypes).  Mirrors include/siren_hip.h one-to-one; the CPU test
+# suite checks that every symbol the header declares is exported.
+_SIGS = {
+    "siren_abi_version": (ctypes.c_int, []),
+    "siren_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "siren_default_splits": (_i32, [_i32, _i32]),
+    "siren_slab_floats": (_i64, [_i32, _i32]),
+    "siren_forward": (ctypes.c_int, [ctypes.POINTER(SirenNet), ctypes.POINTER(SirenBatch), _p]),
+    "siren_train_step": (ctypes.c_int, [ctypes.POINTER(SirenNet), ctypes.POINTER(SirenGrads),
+                                        ctypes.POINTER(SirenBatch), _p]),
+    "siren_backward": (ctypes.c_int, [ctypes.POINTER(SirenNet), ctypes.POINTER(SirenGrads),
+                                      ctypes.POINTER(SirenBatch), _p]),
+    "siren_apply_update": (ctypes.c_int, [ctypes.POINTER(SirenNet), _p, _p, _p, _p, _i64,
+                                          ctypes.POINTER(_p), ctypes.POINTER(_p), ctypes.POINTER(_p),
+                                          _p, _p, ctypes.c_double, _p, _p, _i64, _p]),
+    "siren_coords_fill": (ctypes.c_int, [_p, _i64, _i64, _i64, _p]),
+    "siren_first_fwd": (ctypes.c_int, [_p, _i32, _p, _p, ctypes.c_float, _i32, _i32, _p, _p]),
+    "siren_inner_fwd": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p]),
+    "siren_head_loss": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _i32, ctypes.c_double, _p, _p, _p, _p,
+                                       _p]),
+    "siren_head_bwd": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p]),
+    "siren_inner_bwd_dx": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p]),
+    "siren_first_bwd_dx": (ctypes.c_int, [_p, _p, _p, _i32, _p, _p, ctypes.c_float, _i32, _i32, _p,
+                                          _p]),
+    "siren_inner_bwd_dw": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p]),
+    "siren_dw_reduce": (ctypes.c_int, [_p, _i32, _i32, _p, _i32, _p]),
+    "siren_col_reduce": (ctypes.c_int, [_p, _i64, _i32, _i32, _p, _i32, _i32, _p, _p]),
+    "siren_adam_step": (ctypes.c_int, [_p, _p, _p, _p, _i64, _p, _p]),
+    "siren_plateau_step": (ctypes.c_int, [_p, _p, ctypes.c_double, _p, _p, _i64, _p]),
+    "siren_cast_weight": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p]),
+    "siren_profile_enable": (ctypes.c_int, [_i32]),
+    "siren_profile_reset": (ctypes.c_int, []),
+    "siren_profile_read": (ctypes.c_int, [_i32, ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(_i64)]),
+}
+
+PROF_KINDS = ["first_fwd", "inner_fwd", "head", "bwd_dw", "bwd_dx", "bwd_dx0", "reduce", "update"]
+
+
+def profile_read() -> dict:
+    """{kind: (total_ms, launches)} for every profiled launch kind since the last reset."""
+    lib = load()
+    out = {}
+    for k, name in enumerate(PROF_KINDS):
+        ms, n = ctypes.c_double(0), _i64(0)
+        check(lib.siren_profile_read(k, ctypes.byref(ms), ctypes.byref(n)), "siren_profile_read")
+        out[name] = (ms.value, n.value)
+    return out
+
+_lib = None
+
+
+class SirenError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the native library; raises if it is absent or mismatched."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SirenError(
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (the SIREN path has no eager fallback)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.siren_abi_version() != ABI_VERSION:
+        raise SirenError(f"libsiren_hip ABI {lib.siren_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str = "siren") -> None:
+    """Map a non-zero C-ABI status to SirenError (siren_status_string text)."""
+    if status != 0:
+        msg = load().siren_status_string(status)
+        raise SirenError(f"{what} failed with status {status}: {msg.decode() if msg else '?'}")
+
+
+def ptr(t) -> int:
+    """Device/host address of a torch tensor (0 for None)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,405 @@
+// C-ABI of libsiren_hip.so (include/siren_hip.h): argument validation, the fused
+// training-step launch sequence, and thin wrappers over the individual kernels.
+#include <string.h>
+#include <vector>
+#include "../../include/siren_hip.h"
+#include "siren_kernels.h"
+
+using namespace siren;
+
+static_assert(sizeof(siren_opt_state) == sizeof(OptState), "opt state layout");
+
+namespace {
+
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+inline const bf16* B(const uint16_t* p) { return (const bf16*)p; }
+inline bf16* B(uint16_t* p) { return (bf16*)p; }
+
+#define SIREN_TRY(expr)                        \
+  do {                                         \
+    const hipError_t _e = (expr);              \
+    if (_e != hipSuccess) return (int)_e;      \
+  } while (0)
+
+// ---- optional per-launch HIP-event profiling (bench.py uses it inside its timed region) ----
+struct ProfState {
+  bool on = false;
+  std::vector<hipEvent_t> ev;   // 2 per record
+  std::vector<int> kind;
+  int used = 0;
+};
+ProfState g_prof;
+
+inline void prof_begin(int kind, hipStream_t s) {
+  if (!g_prof.on || g_prof.used >= (int)g_prof.kind.size()) return;
+  (void)hipEventRecord(g_prof.ev[2 * g_prof.used], s);
+  g_prof.kind[g_prof.used] = kind;
+}
+inline void prof_end(hipStream_t s) {
+  if (!g_prof.on || g_prof.used >= (int)g_prof.kind.size()) return;
+  (void)hipEventRecord(g_prof.ev[2 * g_prof.used + 1], s);
+  g_prof.used++;
+}
+
+#define SIREN_PROF(kind, s, expr)            \
+  do {                                       \
+    prof_begin((kind), (s));                 \
+    const hipError_t _pe = (expr);           \
+    prof_end((s));                           \
+    if (_pe != hipSuccess) return _pe;       \
+  } while (0)
+
+bool hidden_ok(int h) { return h >= 128 && h % 128 == 0 && h <= 1024 && 256 % (h / 4) == 0; }
+
+int check_net(const siren_net* n) {
+  if (!n) return SIREN_ERR_NULL;
+  if (n->in_dim < 1 || n->in_dim > 2) return SIREN_ERR_CONFIG;
+  if (!hidden_ok(n->hidden)) return SIREN_ERR_SHAPE;
+  if (n->n_inner < 1 || n->n_inner > SIREN_MAX_INNER) return SIREN_ERR_CONFIG;
+  if (!n->W0 || !n->b0 || !n->w_head || !n->b_head) return SIREN_ERR_NULL;
+  for (int i = 0; i < n->n_inner; ++i)
+    if (!n->b[i] || !n->Wb[i] || !n->WTb[i]) return SIREN_ERR_NULL;
+  return SIREN_OK;
+}
+
+int check_batch(const siren_net* n, const siren_batch* b, bool train) {
+  if (!b) return SIREN_ERR_NULL;
+  if (b->rows <= 0 || b->rows % SIREN_ROW_TILE || b->n_valid < 0 || b->n_valid > b->rows)
+    return SIREN_ERR_SHAPE;
+  if (!b->coords || !b->out || !b->head_part || !b->g || !b->sse_part || !b->gsum_part)
+    return SIREN_ERR_NULL;
+  for (int i = 0; i <= n->n_inner; ++i)
+    if (!b->Y[i] || (i > 0 && !b->C[i])) return SIREN_ERR_NULL;
+  if (train) {
+    if (!b->target || !b->dZ[0] || !b->dZ[1] || !b->col_part || !b->col_part2 || !b->red_tmp ||
+        !b->slab)
+      return SIREN_ERR_NULL;
+    if (b->splits < 1 || b->n_total <= 0) return SIREN_ERR_CONFIG;
+  }
+  return SIREN_OK;
+}
+
+// forward through all layers + head partials; returns hip status
+hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s) {
+  const int R = b->rows, H = n->hidden, L = n->n_inner;
+  SIREN_PROF(SIREN_PROF_FIRST_FWD, s, first_fwd(b->coords, n->in_dim, n->W0, n->b0, n->omega0, R, H, B(b->Y[0]), s));
+  for (int i = 0; i < L; ++i) {
+    NtParams p = {};
+    p.X = B(b->Y[i]);
+    p.W = B(n->Wb[i]);
+    p.M = R; p.N = H; p.K = H;
+    p.omega = n->omega;
+    p.bias = n->b[i];
+    p.Y = B(b->Y[i + 1]);
+    p.C = B(b->C[i + 1]);
+    const bool head = (i == L - 1);
+    p.head_w = n->w_head;
+    p.head_part = b->head_part;
+    SIREN_PROF(SIREN_PROF_INNER_FWD, s, gemm_nt(NT_FWD, head, p, s));
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
+int siren_abi_version(void) { return SIREN_ABI_VERSION; }
+
+const char* siren_status_string(int status) {
+  switch (status) {
+    case SIREN_OK: return "ok";
+    case SIREN_ERR_SHAPE: return "unsupported or inconsistent shape";
+    case SIREN_ERR_NULL: return "required device pointer is NULL";
+    case SIREN_ERR_CONFIG: return "unsupported configuration";
+  }
+  return hipGetErrorString((hipError_t)status);
+}
+
+int32_t siren_default_splits(int32_t rows, int32_t hidden) {
+  // aim for ~1024 blocks (4 per CU at 2 resident per CU) without slices thinner than 8 K-steps
+  const int ntile = (hidden / 128) * (hidden / 128);
+  int splits = 1024 / (ntile > 0 ? ntile : 1);
+  const int nks = rows / 64;
+  const int max_splits = nks / 8 > 0 ? nks / 8 : 1;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  return splits;
+}
+
+int64_t siren_slab_floats(int32_t hidden, int32_t splits) {
+  return (int64_t)splits * hidden * hidden;
+}
+
+int siren_forward(const siren_net* net, siren_batch* batch, void* stream) {
+  int st = check_net(net);
+  if (st) return st;
+  if ((st = check_batch(net, batch, false))) return st;
+  hipStream_t s = S(stream);
+  SIREN_TRY(run_forward(net, batch, s));
+  // out = sum of head partials + bias (g/sse unused at inference: n_valid = 0 path)
+  SIREN_TRY(head_loss(batch->head_part, net->hidden / 128, batch->rows, net->b_head, batch->out,
+                      0, 0.f, batch->out, batch->g, batch->sse_part, batch->gsum_part, s));
+  return SIREN_OK;
+}
+
+static int check_grads(const siren_net* net, const siren_grads* gr) {
+  if (!gr || !gr->W0 || !gr->b0 || !gr->w_head || !gr->b_head) return SIREN_ERR_NULL;
+  for (int i = 0; i < net->n_inner; ++i)
+    if (!gr->W[i] || !gr->b[i]) return SIREN_ERR_NULL;
+  return SIREN_OK;
+}
+
+// autograd of models.py:388-394 given dLoss/dout in batch->g (rows >= n_valid are zero)
+static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch* b, hipStream_t s) {
+  const int R = b->rows, H = net->hidden, L = net->n_inner, in = net->in_dim;
+  SIREN_PROF(SIREN_PROF_HEAD, s, head_bwd(B(b->C[L]), B(b->Y[L]), b->g, net->w_head, net->omega, R, H,
+                                          B(b->dZ[0]), b->col_part, b->col_part2, s));
+  SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part2, H, R / 128, H, gr->w_head, 1, 1, b->red_tmp, s));
+  SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, R / 128, H, gr->b[L - 1], 1, 1, b->red_tmp, s));
+
+  int cur = 0;
+  for (int i = L - 1; i >= 0; --i) {
+    TnParams tp = {};
+    tp.Y = B(b->Y[i]);
+    tp.dZ = B(b->dZ[cur]);
+    tp.R = R; tp.Hin = H; tp.Hout = H;
+    tp.splits = b->splits;
+    tp.slab = b->slab;
+    SIREN_PROF(SIREN_PROF_BWD_DW, s, gemm_tn_dw(tp, s));
+    SIREN_PROF(SIREN_PROF_REDUCE, s, dw_reduce(b->slab, b->splits, H, H, gr->W[i], 1, s));
+
+    NtParams p = {};
+    p.X = B(b->dZ[cur]);
+    p.W = B(net->WTb[i]);
+    p.M = R; p.N = H; p.K = H;
+    p.colsum_part = b->col_part;
+    if (i > 0) {
+      p.omega = net->omega;
+      p.Cprev = B(b->C[i]);
+      p.dZ = B(b->dZ[cur ^ 1]);
+      SIREN_PROF(SIREN_PROF_BWD_DX, s, gemm_nt(NT_DX, false, p, s));
+      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, R / 128, H, gr->b[i - 1], 1, 1, b->red_tmp, s));
+      cur ^= 1;
+    } else {
+      p.omega = net->omega0;
+      p.t = b->coords;
+      p.W0 = net->W0;
+      p.b0 = net->b0;
+      p.in_dim = in;
+      SIREN_PROF(SIREN_PROF_BWD_DX0, s, gemm_nt(NT_DX0, false, p, s));
+      const int64_t rs = (int64_t)(1 + in) * H;
+      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, rs, R / 128, H, gr->b0, 1, 1, b->red_tmp, s));
+      for (int j = 0; j < in; ++j)
+        SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + (int64_t)(1 + j) * H, rs, R / 128, H,
+                                                    gr->W0 + j, in, 1, b->red_tmp, s));
+    }
+  }
+  return SIREN_OK;
+}
+
+int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b, void* stream) {
+  int st = check_net(net);
+  if (st) return st;
+  if ((st = check_batch(net, b, true))) return st;
+  if ((st = check_grads(net, gr))) return st;
+  if (!gr->sse) return SIREN_ERR_NULL;
+  hipStream_t s = S(stream);
+  const int R = b->rows, H = net->hidden;
+
+  if (b->zero_grads && gr->flat) SIREN_TRY(hipMemsetAsync(gr->flat, 0, gr->flat_len * sizeof(float), s));
+
+  // ---- forward (models.py:388-394) + MSE (run.py:168) ----
+  SIREN_TRY(run_forward(net, b, s));
+  const float gscale = (float)(2.0 / b->n_total);  // MSELoss mean backward: 2/N
+  SIREN_PROF(SIREN_PROF_HEAD, s, head_loss(b->head_part, H / 128, R, net->b_head, b->target, b->n_valid,
+                                           gscale, b->out, b->g, b->sse_part, b->gsum_part, s));
+  const int nsum = (R + 255) / 256;
+  SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->sse_part, nsum, gr->sse, 1, s));
+  SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->gsum_part, nsum, gr->b_head, 1, s));
+  // ---- backward (autograd of run.py:185) ----
+  return run_backward(net, gr, b, s);
+}
+
+int siren_backward(const siren_net* net, const siren_grads* gr, siren_batch* b, void* stream) {
+  int st = check_net(net);
+  if (st) return st;
+  if ((st = check_batch(net, b, true))) return st;
+  if ((st = check_grads(net, gr))) return st;
+  hipStream_t s = S(stream);
+  if (b->zero_grads && gr->flat) SIREN_TRY(hipMemsetAsync(gr->flat, 0, gr->flat_len * sizeof(float), s));
+  // bias of the head: sum of g (gsum_part reused as scratch)
+  SIREN_TRY(sum_to(b->g, b->rows, gr->b_head, 1, s));
+  return run_backward(net, gr, b, s);
+}
+
+int siren_apply_update(const siren_net* net, float* params, const float* grads_flat, float* exp_avg,
+                       float* exp_avg_sq, int64_t n_params, float* const* W_fp32, uint16_t* const* Wb,
+                       uint16_t* const* WTb, siren_opt_state* state, const float* sse, double n_total,
+                       float* loss_hist, double* lr_hist, int64_t hist_cap, void* stream) {
+  int st = check_net(net);
+  if (st) return st;
+  if (!params || !grads_flat || !exp_avg || !exp_avg_sq || !state || !sse || !W_fp32 || !Wb || !WTb)
+    return SIREN_ERR_NULL;
+  hipStream_t s = S(stream);
+  SIREN_PROF(SIREN_PROF_UPDATE, s, adam_flat(params, grads_flat, exp_avg, exp_avg_sq, n_params,
+                                             (const OptState*)state, s));
+  for (int i = 0; i < net->n_inner; ++i)
+    SIREN_PROF(SIREN_PROF_UPDATE, s, cast_weight(W_fp32[i], net->hidden, net->hidden, B(Wb[i]), B(WTb[i]), s));
+  SIREN_PROF(SIREN_PROF_UPDATE, s, plateau_step((OptState*)state, sse, n_total, loss_hist, lr_hist, hist_cap, s));
+  return SIREN_OK;
+}
+
+// ---- individual kernels ----------------------------------------------------------------
+
+int siren_coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, void* stream) {
+  if (!t) return SIREN_ERR_NULL;
+  if (rows < 0 || offset < 0 || n_total < 1) return SIREN_ERR_SHAPE;
+  return (int)coords_fill(t, rows, offset, n_total, S(stream));
+}
+
+int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float* b0, float omega0,
+                    int32_t rows, int32_t hidden, uint16_t* Y0, void* stream) {
+  if (!t || !W0 || !b0 || !Y0) return SIREN_ERR_NULL;
+  if (in_dim < 1 || in_dim > 2) return SIREN_ERR_CONFIG;
+  if (rows < 0 || hidden % 4) return SIREN_ERR_SHAPE;
+  return (int)first_fwd(t, in_dim, W0, b0, omega0, rows, hidden, B(Y0), S(stream));
+}
+
+int siren_inner_fwd(const uint16_t* X, const uint16_t* Wb, const float* b, float omega, int32_t rows,
+                    int32_t hidden, uint16_t* Y, uint16_t* C, const float* head_w, float* head_part,
+                    void* stream) {
+  if (!X || !Wb || !b || !Y || !C) return SIREN_ERR_NULL;
+  if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
+  if (head_w && !head_part) return SIREN_ERR_NULL;
+  NtParams p = {};
+  p.X = B(X); p.W = B(Wb); p.M = rows; p.N = hidden; p.K = hidden;
+  p.omega = omega; p.bias = b; p.Y = B(Y); p.C = B(C);
+  p.head_w = head_w; p.head_part = head_part;
+  return (int)gemm_nt(NT_FWD, head_w != nullptr, p, S(stream));
+}
+
+int siren_head_loss(const float* head_part, int32_t nparts, int32_t rows, const float* b_head,
+                    const float* y, int32_t n_valid, double n_total, float* out, float* g,
+                    float* sse_part, float* gsum_part, void* stream) {
+  if (!head_part || !b_head || !out || !g || !sse_part || !gsum_part) return SIREN_ERR_NULL;
+  if (n_valid > 0 && !y) return SIREN_ERR_NULL;
+  if (rows <= 0 || nparts < 1 || n_valid > rows || n_total <= 0) return SIREN_ERR_SHAPE;
+  return (int)head_loss(head_part, nparts, rows, b_head, y, n_valid, (float)(2.0 / n_total), out, g,
+                        sse_part, gsum_part, S(stream));
+}
+
+int siren_head_bwd(const uint16_t* C, const uint16_t* Y, const float* g, const float* w_head,
+                   float omega, int32_t rows, int32_t hidden, uint16_t* dZ, float* db_part,
+                   float* dwh_part, void* stream) {
+  if (!C || !Y || !g || !w_head || !dZ || !db_part || !dwh_part) return SIREN_ERR_NULL;
+  if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
+  return (int)head_bwd(B(C), B(Y), g, w_head, omega, rows, hidden, B(dZ), db_part, dwh_part,
+                       S(stream));
+}
+
+int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTb, const uint16_t* Cprev, float omega_prev,
+                       int32_t rows, int32_t hidden, uint16_t* dZprev, float* db_part, void* stream) {
+  if (!dZ || !WTb || !Cprev || !dZprev || !db_part) return SIREN_ERR_NULL;
+  if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
+  NtParams p = {};
+  p.X = B(dZ); p.W = B(WTb); p.M = rows; p.N = hidden; p.K = hidden;
+  p.omega = omega_prev; p.Cprev = B(Cprev); p.dZ = B(dZprev); p.colsum_part = db_part;
+  return (int)gemm_nt(NT_DX, false, p, S(stream));
+}
+
+int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTb1, const float* t, int32_t in_dim,
+                       const float* W0, const float* b0, float omega0, int32_t rows, int32_t hidden,
+                       float* part, void* stream) {
+  if (!dZ1 || !WTb1 || !t || !W0 || !b0 || !part) return SIREN_ERR_NULL;
+  if (in_dim < 1 || in_dim > 2) return SIREN_ERR_CONFIG;
+  if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
+  NtParams p = {};
+  p.X = B(dZ1); p.W = B(WTb1); p.M = rows; p.N = hidden; p.K = hidden;
+  p.omega = omega0; p.t = t; p.W0 = W0; p.b0 = b0; p.in_dim = in_dim; p.colsum_part = part;
+  return (int)gemm_nt(NT_DX0, false, p, S(stream));
+}
+
+int siren_inner_bwd_dw(const uint16_t* Y, const uint16_t* dZ, int32_t rows, int32_t hidden,
+                       int32_t splits, float* slab, void* stream) {
+  if (!Y || !dZ || !slab) return SIREN_ERR_NULL;
+  if (!hidden_ok(hidden) || rows <= 0 || rows % 64 || splits < 1) return SIREN_ERR_SHAPE;
+  TnParams p = {};
+  p.Y = B(Y); p.dZ = B(dZ); p.R = rows; p.Hin = hidden; p.Hout = hidden; p.splits = splits;
+  p.slab = slab;
+  return (int)gemm_tn_dw(p, S(stream));
+}
+
+int siren_dw_reduce(const float* slab, int32_t splits, int32_t hidden, float* grad, int32_t accumulate,
+                    void* stream) {
+  if (!slab || !grad) return SIREN_ERR_NULL;
+  if (!hidden_ok(hidden) || splits < 1) return SIREN_ERR_SHAPE;
+  return (int)dw_reduce(slab, splits, hidden, hidden, grad, accumulate, S(stream));
+}
+
+int siren_col_reduce(const float* part, int64_t row_stride, int32_t nrows, int32_t ncols, float* out,
+                     int32_t out_stride, int32_t accumulate, float* tmp, void* stream) {
+  if (!part || !out || (nrows > 256 && !tmp)) return SIREN_ERR_NULL;
+  if (nrows < 1 || ncols < 1 || out_stride < 1) return SIREN_ERR_SHAPE;
+  return (int)col_reduce(part, row_stride, nrows, ncols, out, out_stride, accumulate, tmp, S(stream));
+}
+
+int siren_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                    const siren_opt_state* state, void* stream) {
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !state) return SIREN_ERR_NULL;
+  if (n < 0) return SIREN_ERR_SHAPE;
+  return (int)adam_flat(params, grads, exp_avg, exp_avg_sq, n, (const OptState*)state, S(stream));
+}
+
+int siren_plateau_step(siren_opt_state* state, const float* sse, double n_total, float* loss_hist,
+                       double* lr_hist, int64_t hist_cap, void* stream) {
+  if (!state || !sse) return SIREN_ERR_NULL;
+  if (hist_cap > 0 && (!loss_hist || !lr_hist)) return SIREN_ERR_NULL;
+  return (int)plateau_step((OptState*)state, sse, n_total, loss_hist, lr_hist, hist_cap, S(stream));
+}
+
+int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wb, uint16_t* WTb,
+                      void* stream) {
+  if (!W || !Wb || !WTb) return SIREN_ERR_NULL;
+  if (h_out % 64 || h_in % 64) return SIREN_ERR_SHAPE;
+  return (int)cast_weight(W, h_out, h_in, B(Wb), B(WTb), S(stream));
+}
+
+// ---- profiling API ---------------------------------------------------------------------
+int siren_profile_enable(int32_t max_records) {
+  for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);
+  g_prof.ev.clear();
+  g_prof.kind.clear();
+  g_prof.used = 0;
+  g_prof.on = false;
+  if (max_records <= 0) return SIREN_OK;
+  g_prof.ev.resize(2 * (size_t)max_records);
+  for (auto& e : g_prof.ev) SIREN_TRY(hipEventCreate(&e));
+  g_prof.kind.assign(max_records, -1);
+  g_prof.on = true;
+  return SIREN_OK;
+}
+
+int siren_profile_reset(void) {
+  g_prof.used = 0;
+  return SIREN_OK;
+}
+
+int siren_profile_read(int32_t kind, double* total_ms, int64_t* count) {
+  if (!total_ms || !count) return SIREN_ERR_NULL;
+  double tot = 0.0;
+  int64_t n = 0;
+  for (int i = 0; i < g_prof.used; ++i) {
+    if (g_prof.kind[i] != kind) continue;
+    SIREN_TRY(hipEventSynchronize(g_prof.ev[2 * i + 1]));
+    float ms = 0.f;
+    SIREN_TRY(hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]));
+    tot += ms;
+    ++n;
+  }
+  *total_ms = tot;
+  *count = n;
+  return SIREN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,328 @@
+// Memory-bound SIREN kernels: coordinate grid, fp32 first layer, head/MSE, column
+// reductions, fused Adam, ReduceLROnPlateau and the bf16 weight shadows.
+#include <math.h>
+#include "siren_common.h"
+#include "siren_kernels.h"
+
+namespace siren {
+
+static inline int grid_for(int64_t n, int per_block, int cap = 8192) {
+  int64_t g = (n + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// ---------------------------------------------------------------------------------
+// get_coord / torch.linspace(-1, 1, N) (utils.py:99-109), evaluated at global indices
+// [offset, offset+rows): i < N/2 -> -1 + i*step, else 1 - (N-1-i)*step, step = 2/(N-1).
+__global__ void coords_fill_kernel(float* t, int64_t rows, int64_t offset, int64_t n_total) {
+  const float step = (n_total > 1) ? 2.0f / (float)(n_total - 1) : 0.f;
+  const int64_t half = n_total / 2;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = offset + r;
+    float v;
+    if (i >= n_total) v = 0.f;  // padding rows
+    else if (n_total == 1) v = -1.0f;
+    else if (i < half) v = -1.0f + step * (float)i;
+    else v = 1.0f - step * (float)(n_total - 1 - i);
+    t[r] = v;
+  }
+}
+
+hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, hipStream_t s) {
+  hipLaunchKernelGGL(coords_fill_kernel, dim3(grid_for(rows, 256)), dim3(256), 0, s, t, rows, offset,
+                     n_total);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// First SineLayer (is_first=True, models.py:105-115): y0 = sin(omega0 * (t W0^T + b0)).
+// Kept in fp32 end to end: |omega0*z| reaches ~4.4e4 rad at omega0 = 22000, so the
+// pre-activation is formed exactly as torch's CPU addmm rounds it (K=1: one fma;
+// K=2: fma(t1, w1, t0*w0) + b) and sinf does a full-precision range reduction.
+__global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const float* __restrict__ W0,
+                                 const float* __restrict__ b0, float omega0, int R, int H,
+                                 bf16* __restrict__ Y0) {
+  const int hq = H >> 2;
+  const int64_t total = (int64_t)R * hq;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = idx / hq;
+    const int n = (int)(idx - m * hq) * 4;
+    const float t0 = t[m * in_dim];
+    const float t1 = (in_dim > 1) ? t[m * in_dim + 1] : 0.f;
+    float y[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float z;
+      if (in_dim == 1) z = __builtin_fmaf(t0, W0[n + r], b0[n + r]);
+      else z = __builtin_fmaf(t1, W0[(n + r) * 2 + 1], t0 * W0[(n + r) * 2]) + b0[n + r];
+      y[r] = sinf(omega0 * z);
+    }
+    *(bf16x4*)(Y0 + m * H + n) = pack4(y[0], y[1], y[2], y[3]);
+  }
+}
+
+hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
+                     int R, int H, bf16* Y0, hipStream_t s) {
+  if (H % 4 || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(first_fwd_kernel, dim3(grid_for((int64_t)R * (H / 4), 256)), dim3(256), 0, s, t,
+                     in_dim, W0, b0, omega0, R, H, Y0);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// Final nn.Linear(H,1) + MSELoss (models.py:374-381, run.py:125,168):
+//   out = sum_j head_part[j][m] + b;  err = out - y;  g = err * (2/N_total) (0 on pad rows)
+// plus per-block partial sums of err^2 (loss) and g (bias gradient).
+__global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts, int R,
+                                 const float* __restrict__ b_head, const float* __restrict__ y,
+                                 int n_valid, float gscale, float* __restrict__ out,
+                                 float* __restrict__ g, float* __restrict__ sse_part,
+                                 float* __restrict__ gsum_part) {
+  __shared__ float scratch[4];
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  float e2 = 0.f, gv = 0.f;
+  if (m < R) {
+    float o = 0.f;
+    for (int j = 0; j < nparts; ++j) o += head_part[(size_t)j * R + m];
+    o += b_head[0];
+    out[m] = o;
+    if (m < n_valid) {
+      const float err = o - y[m];
+      e2 = err * err;
+      gv = err * gscale;
+    }
+    g[m] = gv;
+  }
+  const float se = block_sum(e2, scratch);
+  const float gs = block_sum(gv, scratch);
+  if (threadIdx.x == 0) {
+    sse_part[blockIdx.x] = se;
+    gsum_part[blockIdx.x] = gs;
+  }
+}
+
+hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_head, const float* y,
+                     int n_valid, float gscale, float* out, float* g, float* sse_part,
+                     float* gsum_part, hipStream_t s) {
+  hipLaunchKernelGGL(head_loss_kernel, dim3((R + 255) / 256), dim3(256), 0, s, head_part, nparts, R,
+                     b_head, y, n_valid, gscale, out, g, sse_part, gsum_part);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// Backward through the head into the last hidden SineLayer:
+//   dY[m][n] = g[m]*w[n];  dZ = (dY * cos) * omega;  db partial = sum_m dZ;
+//   dw_head partial = sum_m g[m]*Y[m][n].     One block per 128 rows.
+__global__ void head_bwd_kernel(const bf16* __restrict__ C, const bf16* __restrict__ Y,
+                                const float* __restrict__ g, const float* __restrict__ w_head,
+                                float omega, int R, int H, bf16* __restrict__ dZ,
+                                float* __restrict__ db_part, float* __restrict__ dwh_part) {
+  __shared__ float red[2][256 * 4];
+  const int hq = H >> 2;            // column quads (divides 256)
+  const int cq = threadIdx.x % hq, rg = threadIdx.x / hq, nrg = blockDim.x / hq;
+  const int n = cq * 4;
+  const float4 w = *(const float4*)(w_head + n);
+  const float wv[4] = {w.x, w.y, w.z, w.w};
+  float db[4] = {0.f, 0.f, 0.f, 0.f}, dw[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t m0 = (int64_t)blockIdx.x * 128;
+  for (int r = rg; r < 128; r += nrg) {
+    const int64_t m = m0 + r;
+    const float gm = g[m];
+    const bf16x4 c = *(const bf16x4*)(C + m * H + n);
+    const bf16x4 yv = *(const bf16x4*)(Y + m * H + n);
+    float dz[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      dz[k] = ((gm * wv[k]) * (float)c[k]) * omega;
+      db[k] += dz[k];
+      dw[k] += gm * (float)yv[k];
+    }
+    *(bf16x4*)(dZ + m * H + n) = pack4(dz[0], dz[1], dz[2], dz[3]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[0][threadIdx.x * 4 + k] = db[k];
+    red[1][threadIdx.x * 4 + k] = dw[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += blockDim.x) {
+    const int q = c >> 2, k = c & 3;
+    float a = 0.f, b = 0.f;
+    for (int gi = 0; gi < nrg; ++gi) {
+      a += red[0][(gi * hq + q) * 4 + k];
+      b += red[1][(gi * hq + q) * 4 + k];
+    }
+    db_part[(size_t)blockIdx.x * H + c] = a;
+    dwh_part[(size_t)blockIdx.x * H + c] = b;
+  }
+}
+
+hipError_t head_bwd(const bf16* C, const bf16* Y, const float* g, const float* w_head, float omega,
+                    int R, int H, bf16* dZ, float* db_part, float* dwh_part, hipStream_t s) {
+  if (R % 128 || H % 4 || 256 % (H / 4)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(R / 128), dim3(256), 0, s, C, Y, g, w_head, omega, R, H,
+                     dZ, db_part, dwh_part);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// Deterministic column reduction of partial rows, two passes of the same kernel:
+// pass 1 sums row chunks into tmp[64][ncols], pass 2 sums those 64 rows.
+__global__ void col_reduce_kernel(const float* __restrict__ part, int64_t row_stride, int nrows,
+                                  int ncols, float* __restrict__ out, int64_t out_row_stride,
+                                  int out_stride, int accumulate) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int chunk = blockIdx.y, nchunk = gridDim.y;
+  const int r0 = (int)(((int64_t)chunk * nrows) / nchunk);
+  const int r1 = (int)(((int64_t)(chunk + 1) * nrows) / nchunk);
+  float s = 0.f;
+  if (col < ncols)
+    for (int r = r0 + rg; r < r1; r += 4) s += part[(int64_t)r * row_stride + col];
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && col < ncols) {
+    const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    float* o = out + (int64_t)chunk * out_row_stride + (int64_t)col * out_stride;
+    *o = accumulate ? (*o + v) : v;
+  }
+}
+
+hipError_t col_reduce(const float* part, int64_t row_stride, int nrows, int ncols, float* out,
+                      int out_stride, int accumulate, float* tmp, hipStream_t s) {
+  const int cb = (ncols + 63) / 64;
+  if (nrows <= 256) {
+    hipLaunchKernelGGL(col_reduce_kernel, dim3(cb, 1), dim3(256), 0, s, part, row_stride, nrows, ncols,
+                       out, (int64_t)0, out_stride, accumulate);
+    return hipGetLastError();
+  }
+  const int chunks = 64;
+  hipLaunchKernelGGL(col_reduce_kernel, dim3(cb, chunks), dim3(256), 0, s, part, row_stride, nrows,
+                     ncols, tmp, (int64_t)ncols, 1, 0);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3(cb, 1), dim3(256), 0, s, (const float*)tmp, (int64_t)ncols,
+                     chunks, ncols, out, (int64_t)0, out_stride, accumulate);
+  return hipGetLastError();
+}
+
+// out[0] (+)= sum(x[0..n))  -- single block, fixed order.
+__global__ void sum_to_kernel(const float* __restrict__ x, int n, float* out, int accumulate) {
+  __shared__ float scratch[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[i];
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + s : s;
+}
+
+hipError_t sum_to(const float* x, int n, float* out, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(sum_to_kernel, dim3(1), dim3(1024), 0, s, x, n, out, accumulate);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// torch.optim.Adam step (run.py:116,186) over the flat fp32 parameter vector, following
+// the CUDA reference's per-element rounding:
+//   m = fma(1-b1, g-m, m)                      (lerp, small weight)
+//   v = fma((1-b2)*g, g, v*b2)                 (mul_ + addcmul_)
+//   d = sqrt(v) / sqrt(bc2) + eps              (correctly rounded sqrt/div)
+//   p = p + ((-lr/bc1) * m) / d                (addcdiv_)
+// bias corrections in fp64 from the device step counter.
+__global__ void adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                 float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                 const OptState* __restrict__ st) {
+#pragma clang fp contract(off)
+  const double step = st->step + 1.0;
+  const double bc1 = 1.0 - pow(st->beta1, step);
+  const double bc2 = 1.0 - pow(st->beta2, step);
+  const float neg_step_size = (float)((st->lr / bc1) * -1.0);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  const float w1 = (float)(1.0 - st->beta1);
+  const float b2 = (float)st->beta2;
+  const float w2 = (float)(1.0 - st->beta2);
+  const float eps = (float)st->eps;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    float mi = m[i], vi = v[i];
+    mi = __builtin_fmaf(w1, gi - mi, mi);
+    vi = __builtin_fmaf(w2 * gi, gi, vi * b2);
+    const float d = __fsqrt_rn(vi) / bc2_sqrt + eps;
+    p[i] = p[i] + (neg_step_size * mi) / d;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+hipError_t adam_flat(float* p, const float* g, float* m, float* v, int64_t n, const OptState* st,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(adam_flat_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, p, g, m, v, n,
+                     st);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// ReduceLROnPlateau(mode='min', factor, patience, threshold=1e-4 rel, min_lr, eps=1e-8)
+// .step(loss) (run.py:117,187) on device, after Adam used the current lr.  Also bumps the
+// Adam step counter and records (loss, lr) history for the host to fetch lazily.
+__global__ void plateau_kernel(OptState* st, const float* sse, double n_total, float* loss_hist,
+                               double* lr_hist, int64_t hist_cap) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const float loss = (float)((double)sse[0] / n_total);
+  const double cur = (double)loss;
+  const int64_t k = (int64_t)st->step;  // index of this optimizer step (0-based)
+  st->step = st->step + 1.0;
+  st->last_epoch += 1;
+  if (cur < st->best * (1.0 - st->threshold)) {
+    st->best = cur;
+    st->num_bad = 0;
+  } else {
+    st->num_bad += 1;
+  }
+  if (st->num_bad > st->patience) {
+    const double old_lr = st->lr;
+    const double new_lr = fmax(old_lr * st->factor, st->min_lr);
+    if (old_lr - new_lr > st->eps_lr) st->lr = new_lr;
+    st->num_bad = 0;
+  }
+  if (k >= 0 && k < hist_cap) {
+    loss_hist[k] = loss;
+    lr_hist[k] = st->lr;
+  }
+}
+
+hipError_t plateau_step(OptState* st, const float* sse, double n_total, float* loss_hist,
+                        double* lr_hist, int64_t hist_cap, hipStream_t s) {
+  hipLaunchKernelGGL(plateau_kernel, dim3(1), dim3(64), 0, s, st, sse, n_total, loss_hist, lr_hist,
+                     hist_cap);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// bf16 shadows of a hidden weight W[o][k] (fp32 master): Wb = W, WTb = W^T, through a
+// 64x64 LDS transpose so both stores are coalesced.
+__global__ void cast_weight_kernel(const float* __restrict__ W, int H_out, int H_in,
+                                   bf16* __restrict__ Wb, bf16* __restrict__ WTb) {
+  __shared__ float tile[64][65];
+  const int o0 = blockIdx.y * 64, k0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 64 x 4
+  for (int r = ty; r < 64; r += 4) {
+    const float w = W[(size_t)(o0 + r) * H_in + k0 + tx];
+    tile[r][tx] = w;
+    Wb[(size_t)(o0 + r) * H_in + k0 + tx] = (bf16)w;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) WTb[(size_t)(k0 + r) * H_out + o0 + tx] = (bf16)tile[tx][r];
+}
+
+hipError_t cast_weight(const float* W, int H_out, int H_in, bf16* Wb, bf16* WTb, hipStream_t s) {
+  if (H_out % 64 || H_in % 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cast_weight_kernel, dim3(H_in / 64, H_out / 64), dim3(256), 0, s, W, H_out, H_in,
+                     Wb, WTb);
+  return hipGetLastError();
+}
+
+}  // namespace siren

@@ -1,0 +1,81 @@
+// Internal host-side launchers for the SIREN gfx950 kernels (not the public C-ABI;
+// that lives in include/siren_hip.h and capi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace siren {
+
+typedef __bf16 bf16;
+
+enum NtMode { NT_FWD = 0, NT_DX = 1, NT_DX0 = 2 };
+
+struct NtParams {
+  const bf16* X;  // [M][K]
+  const bf16* W;  // [N][K]
+  int M, N, K;
+  float omega;  // FWD: this layer's omega; DX: omega of the layer below; DX0: omega_0
+  // NT_FWD
+  const float* bias;    // [N]
+  bf16* Y;              // [M][N]
+  bf16* C;              // [M][N]
+  const float* head_w;  // [N]          (HEAD only)
+  float* head_part;     // [N/128][M]   (HEAD only)
+  // NT_DX / NT_DX0
+  const bf16* Cprev;    // [M][N]  cos of the layer below (NT_DX)
+  bf16* dZ;             // [M][N]  (NT_DX)
+  float* colsum_part;   // NT_DX: [M/128][N];  NT_DX0: [M/128][1+in][N]
+  // NT_DX0
+  const float* t;       // [M][in]
+  const float* W0;      // [N][in]
+  const float* b0;      // [N]
+  int in_dim;
+};
+
+hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s);
+
+struct TnParams {
+  const bf16* Y;   // [R][Hin]   layer input (A role: dW column index k)
+  const bf16* dZ;  // [R][Hout]  layer pre-activation gradient (B role: dW row index o)
+  int R, Hin, Hout;
+  int splits;
+  float* slab;     // [splits][Hout*Hin] fp32 in MFMA-native order (see dw_reduce)
+};
+
+hipError_t gemm_tn_dw(const TnParams& p, hipStream_t s);
+// grad[o][k] (+)= sum_s slab[s]  (grad row-major [Hout][Hin])
+hipError_t dw_reduce(const float* slab, int splits, int Hin, int Hout, float* grad, int accumulate,
+                     hipStream_t s);
+
+// elementwise / reduction kernels (elementwise.hip)
+hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, hipStream_t s);
+hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
+                     int R, int H, bf16* Y0, hipStream_t s);
+hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_head, const float* y,
+                     int n_valid, float gscale, float* out, float* g, float* sse_part,
+                     float* gsum_part, hipStream_t s);
+hipError_t head_bwd(const bf16* C, const bf16* Y, const float* g, const float* w_head, float omega,
+                    int R, int H, bf16* dZ, float* db_part, float* dwh_part, hipStream_t s);
+// out[c*out_stride] (+)= sum_r part[r*row_stride + c]; tmp holds >= 64*ncols floats
+hipError_t col_reduce(const float* part, int64_t row_stride, int nrows, int ncols, float* out,
+                      int out_stride, int accumulate, float* tmp, hipStream_t s);
+
+struct OptState {      // device-resident optimizer + ReduceLROnPlateau state (run.py:116-117)
+  double lr;           // current learning rate (param_groups[0]['lr'])
+  double best;         // plateau: best loss so far (init +inf)
+  double step;         // Adam step count (torch keeps it as a float tensor)
+  int32_t num_bad;     // plateau: num_bad_epochs
+  int32_t last_epoch;  // number of scheduler.step() calls
+  double min_lr, factor, threshold, eps_lr;
+  int32_t patience, pad0;
+  double beta1, beta2, eps;
+};
+
+hipError_t adam_flat(float* p, const float* g, float* m, float* v, int64_t n, const OptState* st,
+                     hipStream_t s);
+hipError_t plateau_step(OptState* st, const float* sse, double n_total, float* loss_hist,
+                        double* lr_hist, int64_t hist_cap, hipStream_t s);
+hipError_t cast_weight(const float* W, int H_out, int H_in, bf16* Wb, bf16* WTb, hipStream_t s);
+hipError_t sum_to(const float* x, int n, float* out, int accumulate, hipStream_t s);
+
+}  // namespace siren

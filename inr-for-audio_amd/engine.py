@@ -1,0 +1,376 @@
+"""Device-resident SIREN training engine over the libsiren_hip C-ABI.
+
+Replaces what run.py's hot loop (run.py:156-190) does through torch eager + autograd:
+forward, MSELoss, backward, Adam, ReduceLROnPlateau.  The engine owns
+
+* a flat fp32 parameter vector (plus grad / exp_avg / exp_avg_sq vectors of the same
+  layout) whose segments the nn.Module parameters are re-pointed at, so
+  ``model.state_dict()`` always shows the live weights;
+* bf16 shadows W_i and W_i^T of every hidden weight (refreshed by the update kernel);
+* one micro-batch workspace (bf16 activations Y_i = sin, C_i = cos, dZ ping-pong and fp32
+  partial-sum slabs), reused for every micro-batch of the full-batch step;
+* the optimizer / scheduler state as a device struct, so a step needs no host sync and
+  can be captured in a HIP graph.
+
+Data parallel: one process per GPU (torchrun), rank r owns the contiguous coordinate slice
+[r*N/G, (r+1)*N/G); the MSE gradient uses the GLOBAL N and the flat gradient vector (whose
+tail slot carries the summed squared error) is all-reduced once per step.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import MAX_INNER, ROW_TILE, SirenBatch, SirenGrads, SirenNet, SirenOptState, check, ptr
+
+SEG_ALIGN = 64  # floats: every flat segment starts 256-B aligned
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class NetSpec:
+    in_dim: int
+    hidden: int
+    n_inner: int
+    omega0: float
+    omega: float
+
+
+def net_spec(model) -> NetSpec:
+    """Validate that `model` is the sine-only SirenWithSnakeTanh the HIP path implements."""
+    spec = getattr(model, "hip_spec", None)
+    if spec is None:
+        raise TypeError("expected inr_for_audio_amd.models.SirenWithSnakeTanh")
+    return spec()
+
+
+class ParamLayout:
+    """Offsets of every parameter (named_parameters order == state_dict order == the
+    order torch.optim.Adam indexes its state) inside the flat fp32 vectors."""
+
+    def __init__(self, model):
+        self.names, self.shapes, self.offsets, self.numels = [], [], [], []
+        off = 0
+        for name, p in model.named_parameters():
+            self.names.append(name)
+            self.shapes.append(tuple(p.shape))
+            self.offsets.append(off)
+            self.numels.append(p.numel())
+            off = round_up(off + p.numel(), SEG_ALIGN)
+        self.n_params = off                   # Adam runs over [0, n_params)
+        self.sse_offset = off                 # summed squared error rides the all-reduce
+        self.flat_len = off + SEG_ALIGN
+
+    def view(self, flat: torch.Tensor, i: int) -> torch.Tensor:
+        o = self.offsets[i]
+        return flat[o:o + self.numels[i]].view(self.shapes[i])
+
+
+class Workspace:
+    """Activations + scratch for `rows` coordinates (rows % 128 == 0)."""
+
+    def __init__(self, spec: NetSpec, rows: int, device, train: bool = True, splits: int | None = None):
+        lib = _lib.load()
+        if rows % ROW_TILE:
+            raise ValueError(f"rows={rows} must be a multiple of {ROW_TILE}")
+        H, L, R = spec.hidden, spec.n_inner, rows
+        bf, f32 = torch.bfloat16, torch.float32
+        e = lambda *s, dtype=f32: torch.empty(*s, dtype=dtype, device=device)  # noqa: E731
+        self.rows = R
+        self.Y = [e(R, H, dtype=bf) for _ in range(L + 1)]
+        self.C = [None] + [e(R, H, dtype=bf) for _ in range(L)]
+        self.out = e(R)
+        self.g = torch.zeros(R, dtype=f32, device=device)
+        self.head_part = e(H // 128, R)
+        nsum = (R + 255) // 256
+        self.sse_part = e(nsum)
+        self.gsum_part = e(nsum)
+        self.train = train
+        if train:
+            self.splits = int(splits or lib.siren_default_splits(R, H))
+            self.dZ = [e(R, H, dtype=bf) for _ in range(2)]
+            self.col_part = e(R // 128, 1 + spec.in_dim, H)
+            self.col_part2 = e(R // 128, H)
+            self.red_tmp = e(64, H)
+            self.slab = e(int(lib.siren_slab_floats(H, self.splits)))
+        else:
+            self.splits = 1
+            self.dZ = [None, None]
+            self.col_part = self.col_part2 = self.red_tmp = self.slab = None
+
+    def batch(self, coords: torch.Tensor, target, n_valid: int, n_total: float,
+              zero_grads: bool = False) -> SirenBatch:
+        b = SirenBatch()
+        b.rows, b.n_valid, b.n_total = self.rows, int(n_valid), float(n_total)
+        b.splits, b.zero_grads = self.splits, int(zero_grads)
+        b.coords, b.target = ptr(coords), ptr(target)
+        for i, y in enumerate(self.Y):
+            b.Y[i] = ptr(y)
+        for i, c in enumerate(self.C):
+            b.C[i] = ptr(c)
+        b.dZ[0], b.dZ[1] = ptr(self.dZ[0]), ptr(self.dZ[1])
+        b.out, b.g, b.head_part = ptr(self.out), ptr(self.g), ptr(self.head_part)
+        b.sse_part, b.gsum_part = ptr(self.sse_part), ptr(self.gsum_part)
+        b.col_part, b.col_part2 = ptr(self.col_part), ptr(self.col_part2)
+        b.red_tmp, b.slab = ptr(self.red_tmp), ptr(self.slab)
+        return b
+
+
+def make_net(spec: NetSpec, W0, b0, bs, Wbs, WTbs, w_head, b_head) -> SirenNet:
+    n = SirenNet()
+    n.in_dim, n.hidden, n.n_inner = spec.in_dim, spec.hidden, spec.n_inner
+    n.omega0, n.omega = spec.omega0, spec.omega
+    n.W0, n.b0 = ptr(W0), ptr(b0)
+    for i in range(spec.n_inner):
+        n.b[i], n.Wb[i], n.WTb[i] = ptr(bs[i]), ptr(Wbs[i]), ptr(WTbs[i])
+    n.w_head, n.b_head = ptr(w_head), ptr(b_head)
+    return n
+
+
+def make_grads(spec: NetSpec, layout: ParamLayout, gflat: torch.Tensor) -> SirenGrads:
+    g = SirenGrads()
+    v = lambda i: layout.view(gflat, i)  # noqa: E731
+    L = spec.n_inner
+    g.W0, g.b0 = ptr(v(0)), ptr(v(1))
+    for i in range(L):
+        g.W[i], g.b[i] = ptr(v(2 + 2 * i)), ptr(v(3 + 2 * i))
+    g.w_head, g.b_head = ptr(v(2 + 2 * L)), ptr(v(3 + 2 * L))
+    g.sse = gflat.data_ptr() + 4 * layout.sse_offset
+    g.flat, g.flat_len = ptr(gflat), layout.flat_len
+    return g
+
+
+def cast_shadows(spec, Ws, Wbs, WTbs, stream):
+    lib = _lib.load()
+    for W, Wb, WTb in zip(Ws, Wbs, WTbs):
+        check(lib.siren_cast_weight(ptr(W), spec.hidden, spec.hidden, ptr(Wb), ptr(WTb), stream),
+              "siren_cast_weight")
+
+
+def _dist():
+    d = torch.distributed
+    if d.is_available() and d.is_initialized() and d.get_world_size() > 1:
+        return d
+    return None
+
+
+def shard_range(n_total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous coordinate slice owned by `rank`."""
+    return n_total * rank // world, n_total * (rank + 1) // world
+
+
+class SirenEngine:
+    """Full-batch SIREN fit on one GPU (or one DP rank): run.py:108-190 minus the plots."""
+
+    def __init__(self, model, coords: torch.Tensor, target: torch.Tensor, *, lr: float = 1e-3,
+                 min_lr: float = 1e-6, factor: float = 0.8, patience: int = 200,
+                 n_total: int | None = None, micro_batch: int = 1 << 20, hist_cap: int = 20000,
+                 splits: int | None = None, device=None):
+        lib = _lib.load()
+        self.lib = lib
+        self.device = torch.device(device or "cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("SirenEngine runs on the GPU only (HIP kernels; no CPU fallback)")
+        self.model = model
+        self.spec = spec = net_spec(model)
+        self.layout = lay = ParamLayout(model)
+        dev = self.device
+
+        # flat fp32 parameter storage; module parameters become views into it
+        self.params = torch.zeros(lay.flat_len, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for i, (_, p) in enumerate(model.named_parameters()):
+                lay.view(self.params, i).copy_(p.detach().to(dev, torch.float32))
+        d = _dist()
+        if d is not None:
+            d.broadcast(self.params, src=0)
+        for i, (_, p) in enumerate(model.named_parameters()):
+            p.data = lay.view(self.params, i)
+        self.grads = torch.zeros_like(self.params)
+        self.exp_avg = torch.zeros_like(self.params)
+        self.exp_avg_sq = torch.zeros_like(self.params)
+
+        L, H = spec.n_inner, spec.hidden
+        pv = lambda i: lay.view(self.params, i)  # noqa: E731
+        self.W = [pv(2 + 2 * i) for i in range(L)]
+        self.Wb = [torch.empty(H, H, dtype=torch.bfloat16, device=dev) for _ in range(L)]
+        self.WTb = [torch.empty(H, H, dtype=torch.bfloat16, device=dev) for _ in range(L)]
+        self.net = make_net(spec, pv(0), pv(1), [pv(3 + 2 * i) for i in range(L)], self.Wb, self.WTb,
+                            pv(2 + 2 * L), pv(3 + 2 * L))
+        self.grad_struct = make_grads(spec, lay, self.grads)
+        self._Wp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.W])
+        self._Wbp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.Wb])
+        self._WTbp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.WTb])
+
+        # optimizer + scheduler state (torch defaults of run.py:116-117)
+        st = SirenOptState()
+        st.lr, st.best, st.step = float(lr), math.inf, 0.0
+        st.num_bad, st.last_epoch = 0, 0
+        st.min_lr, st.factor, st.threshold, st.eps_lr = float(min_lr), float(factor), 1e-4, 1e-8
+        st.patience = int(patience)
+        st.beta1, st.beta2, st.eps = 0.9, 0.999, 1e-8
+        self.state = torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(dev)
+        self.hist_cap = int(hist_cap)
+        self.loss_hist = torch.zeros(max(self.hist_cap, 1), dtype=torch.float32, device=dev)
+        self.lr_hist = torch.zeros(max(self.hist_cap, 1), dtype=torch.float64, device=dev)
+
+        # data: this rank's contiguous shard, padded per micro-batch
+        coords = coords.reshape(-1, spec.in_dim).to(torch.float32)
+        target = target.reshape(-1).to(torch.float32)
+        n_global = coords.shape[0] if n_total is None else int(n_total)
+        rank, world = (d.get_rank(), d.get_world_size()) if d is not None else (0, 1)
+        if n_total is None and world > 1:
+            lo, hi = shard_range(n_global, rank, world)
+            coords, target = coords[lo:hi], target[lo:hi]
+        self.n_total = n_global
+        self.n_local = n = coords.shape[0]
+        mb = min(round_up(int(micro_batch), ROW_TILE), round_up(max(n, 1), ROW_TILE))
+        self.rows = mb
+        self.n_micro = max(1, -(-n // mb))
+        padded = self.n_micro * mb
+        self.coords = torch.zeros(padded, spec.in_dim, dtype=torch.float32, device=dev)
+        self.target = torch.zeros(padded, dtype=torch.float32, device=dev)
+        self.coords[:n] = coords.to(dev)
+        self.target[:n] = target.to(dev)
+        self.ws = Workspace(spec, mb, dev, train=True, splits=splits)
+        self.batches = []
+        for k in range(self.n_micro):
+            lo = k * mb
+            c = self.coords[lo:lo + mb]
+            t = self.target[lo:lo + mb]
+            self.batches.append(self.ws.batch(c, t, min(mb, n - lo), n_global, zero_grads=(k == 0)))
+        self.steps_done = 0
+        self.graph = None
+        self._refresh_shadows()
+
+    # ------------------------------------------------------------------ internals
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _refresh_shadows(self):
+        cast_shadows(self.spec, self.W, self.Wb, self.WTb, self._stream())
+
+    def _launch_grads(self):
+        s = self._stream()
+        for b in self.batches:
+            check(self.lib.siren_train_step(ctypes.byref(self.net), ctypes.byref(self.grad_struct),
+                                            ctypes.byref(b), s), "siren_train_step")
+
+    def _launch_update(self):
+        check(self.lib.siren_apply_update(
+            ctypes.byref(self.net), ptr(self.params), ptr(self.grads), ptr(self.exp_avg),
+            ptr(self.exp_avg_sq), self.layout.n_params, self._Wp, self._Wbp, self._WTbp,
+            ptr(self.state), self.grads.data_ptr() + 4 * self.layout.sse_offset, float(self.n_total),
+            ptr(self.loss_hist), ptr(self.lr_hist), self.hist_cap, self._stream()),
+            "siren_apply_update")
+
+    # ------------------------------------------------------------------ public API
+    def step(self):
+        """One optimizer step over the full batch (all micro-batches, all ranks)."""
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._launch_grads()
+            d = _dist()
+            if d is not None:
+                d.all_reduce(self.grads)
+            self._launch_update()
+        self.steps_done += 1
+
+    def capture_graph(self, warmup: int = 0):
+        """Capture one whole step as a HIP graph (single-process only)."""
+        if _dist() is not None:
+            raise RuntimeError("graph capture is for the single-GPU path")
+        for _ in range(warmup):
+            self.step()
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self._launch_grads()
+                self._launch_update()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.graph = g
+        return g
+
+    def opt_state(self) -> SirenOptState:
+        return SirenOptState.from_buffer_copy(bytes(self.state.cpu().numpy().tobytes()))
+
+    def history(self):
+        """(losses, lrs) of the steps done so far (host copies)."""
+        k = min(self.steps_done, self.hist_cap)
+        return self.loss_hist[:k].cpu().numpy(), self.lr_hist[:k].cpu().numpy()
+
+    def last_loss(self) -> float:
+        k = min(self.steps_done, self.hist_cap) - 1
+        return float(self.loss_hist[k].item()) if k >= 0 else float("nan")
+
+    def grad_views(self):
+        return [self.layout.view(self.grads, i) for i in range(len(self.layout.names))]
+
+    @torch.no_grad()
+    def infer(self, coords: torch.Tensor, chunk: int | None = None) -> torch.Tensor:
+        """model(coords) with the current weights (run.py:249-256); returns [N] fp32."""
+        return forward_net(self.spec, self.net, coords.reshape(-1, self.spec.in_dim), self.device,
+                           chunk or self.rows, shadows_ready=True)
+
+    def adam_state_dict(self):
+        """torch.optim.Adam-compatible state_dict (run.py:359-362 checkpoint format)."""
+        st = self.opt_state()
+        state = {}
+        for i in range(len(self.layout.names)):
+            state[i] = {
+                "step": torch.tensor(float(st.step)),
+                "exp_avg": self.layout.view(self.exp_avg, i).detach().cpu().clone(),
+                "exp_avg_sq": self.layout.view(self.exp_avg_sq, i).detach().cpu().clone(),
+            }
+        group = {"lr": float(st.lr), "betas": (st.beta1, st.beta2), "eps": st.eps, "weight_decay": 0,
+                 "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                 "differentiable": False, "fused": None, "decoupled_weight_decay": False,
+                 "params": list(range(len(self.layout.names)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_adam_state_dict(self, sd):
+        """Resume from a reference checkpoint's optimizer_state_dict (run.py:104-105)."""
+        with torch.no_grad():
+            step = 0.0
+            for i in range(len(self.layout.names)):
+                s = sd["state"].get(i)
+                if s is None:
+                    continue
+                self.layout.view(self.exp_avg, i).copy_(s["exp_avg"].reshape(self.layout.shapes[i]))
+                self.layout.view(self.exp_avg_sq, i).copy_(s["exp_avg_sq"].reshape(self.layout.shapes[i]))
+                step = float(s["step"])
+            st = self.opt_state()
+            st.step = step
+            st.lr = float(sd["param_groups"][0]["lr"])
+            self.state.copy_(torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(self.device))
+
+
+def forward_net(spec: NetSpec, net: SirenNet, coords: torch.Tensor, device, chunk: int,
+                shadows_ready: bool = True) -> torch.Tensor:
+    """Inference through siren_forward in chunks of `chunk` rows."""
+    lib = _lib.load()
+    n = coords.shape[0]
+    chunk = min(round_up(chunk, ROW_TILE), round_up(max(n, 1), ROW_TILE))
+    ws = Workspace(spec, chunk, device, train=False)
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    buf = torch.zeros(chunk, spec.in_dim, dtype=torch.float32, device=device)
+    s = torch.cuda.current_stream(device).cuda_stream
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        buf.zero_()
+        buf[:hi - lo] = coords[lo:hi].to(device, torch.float32)
+        b = ws.batch(buf, None, 0, 1.0)
+        check(lib.siren_forward(ctypes.byref(net), ctypes.byref(b), s), "siren_forward")
+        out[lo:hi] = ws.out[:hi - lo]
+    return out

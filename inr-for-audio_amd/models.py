@@ -1,0 +1,196 @@
+"""SIREN modules with the reference's constructor API, parameter names and init
+(models.py:84-120 SineLayer, models.py:306-394 SirenWithSnakeTanh), computing on the
+gfx950 HIP kernels.
+
+Parameters are created with exactly the reference's torch calls in the reference's order
+(nn.Linear default init, then the SIREN re-draw), so ``torch.manual_seed(s)`` gives
+bit-identical weights and the state_dict keys (``net.{i}.linear.weight`` ...,
+``net.{L+1}.weight``) load into either implementation.
+
+``forward`` runs the fused HIP forward and has a HIP backward (autograd.Function), so a
+user loop of ``model(x)`` / ``loss.backward()`` / ``torch.optim.Adam`` works as a drop-in.
+The fast path for fitting is ``engine.SirenEngine`` (used by ``run.train``).  There is no
+eager fallback: CPU tensors or unsupported configurations raise.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+
+
+class SineLayer(nn.Module):
+    """sin(omega_0 * Linear(x)) -- models.py:84-120 (init: models.py:105-112)."""
+
+    def __init__(self, in_features, out_features, bias=True, is_first=False, omega_0=30):
+        super().__init__()
+        self.omega_0 = omega_0
+        self.is_first = is_first
+        self.in_features = in_features
+        self.linear = nn.Linear(in_features, out_features, bias=bias)
+        self.init_weights()
+
+    def init_weights(self):
+        with torch.no_grad():
+            if self.is_first:
+                self.linear.weight.uniform_(-1 / self.in_features, 1 / self.in_features)
+            else:
+                self.linear.weight.uniform_(-np.sqrt(6 / self.in_features) / self.omega_0,
+                                            np.sqrt(6 / self.in_features) / self.omega_0)
+
+    def forward(self, input):
+        raise NotImplementedError(
+            "a lone SineLayer has no HIP kernel: wrap it in SirenWithSnakeTanh (fused path)")
+
+    def forward_with_intermediate(self, input):
+        raise NotImplementedError("activation inspection is not part of the HIP path")
+
+
+class Snake(nn.Module):
+    """Parameter-compatible Snake (models.py:185-241): y = x + sin^2(a x)/a.  The fused
+    Snake epilogue is a later row of the hot-path table; it has no
+    kernel yet, so forward raises."""
+
+    def __init__(self, in_features, a=None, trainable=True):
+        super().__init__()
+        self.in_features = in_features if isinstance(in_features, list) else [in_features]
+        initial_a = torch.ones(self.in_features) * (a if a is not None else 1.0)
+        self.a = nn.Parameter(initial_a)
+        self.a.requires_grad = trainable
+
+    def forward(self, x):
+        raise NotImplementedError("Snake epilogue not implemented on the HIP path yet (SURVEY §8 f3)")
+
+
+class SirenWithSnakeTanh(nn.Module):
+    """MLP with sine / Snake / Tanh activations -- models.py:306-394.  The HIP path covers
+    the SIREN configuration (first SineLayer, num_sine hidden SineLayers, final Linear)."""
+
+    def __init__(self, in_features, out_features, hidden_features, num_sine, num_snake, num_tanh,
+                 first_linear=False, last_linear=True, first_omega_0=30, hidden_omega_0=30.,
+                 a_initial=50, num_freq=None, scale=2.0):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.hidden_features = hidden_features
+        self.num_sine, self.num_snake, self.num_tanh = num_sine, num_snake, num_tanh
+        self.first_linear, self.last_linear = first_linear, last_linear
+        self.first_omega_0, self.hidden_omega_0 = first_omega_0, hidden_omega_0
+        net = []
+        if first_linear:
+            net.append(nn.Linear(in_features, hidden_features))
+            net.append(Snake(hidden_features, a=a_initial))
+        else:
+            net.append(SineLayer(in_features, hidden_features, is_first=True, omega_0=first_omega_0))
+        for _ in range(num_sine):
+            net.append(SineLayer(hidden_features, hidden_features, is_first=False,
+                                 omega_0=hidden_omega_0))
+        for _ in range(num_snake):
+            net.append(nn.Linear(hidden_features, hidden_features))
+            net.append(Snake(hidden_features, a=a_initial))
+        for _ in range(num_tanh):
+            net.append(nn.Linear(hidden_features, hidden_features))
+            net.append(nn.Tanh())
+        if last_linear:
+            final_linear = nn.Linear(hidden_features, out_features)
+            with torch.no_grad():
+                final_linear.weight.uniform_(-np.sqrt(6 / hidden_features) / hidden_omega_0,
+                                             np.sqrt(6 / hidden_features) / hidden_omega_0)
+            net.append(final_linear)
+        else:
+            net.append(SineLayer(hidden_features, out_features, is_first=False,
+                                 omega_0=hidden_omega_0))
+        self.net = nn.Sequential(*net)
+
+    def hip_spec(self):
+        """NetSpec of the fused path; raises for configurations it does not cover."""
+        from .engine import NetSpec
+        if self.first_linear or self.num_snake or self.num_tanh or not self.last_linear:
+            raise NotImplementedError(
+                "HIP path covers the SIREN configuration only (first_linear=False, num_snake=0, "
+                "num_tanh=0, last_linear=True); Snake/Tanh epilogues are SURVEY §8 f3")
+        if self.out_features != 1:
+            raise NotImplementedError("HIP path: out_features must be 1 (run.py:95,112)")
+        if self.num_sine < 1:
+            raise NotImplementedError("HIP path: num_sine must be >= 1")
+        if self.in_features not in (1, 2):
+            raise NotImplementedError("HIP path: in_features must be 1 or 2")
+        H = self.hidden_features
+        if H % 128 or H > 1024 or 256 % (H // 4):
+            raise NotImplementedError(f"HIP path: hidden_features must be 128/256/512/1024, got {H}")
+        if self.num_sine > _lib.MAX_INNER:
+            raise NotImplementedError(f"HIP path: num_sine <= {_lib.MAX_INNER}")
+        return NetSpec(self.in_features, H, self.num_sine, float(self.first_omega_0),
+                       float(self.hidden_omega_0))
+
+    def forward(self, coords):
+        """(1, N, in) or (N, in) CUDA coords -> (..., N, 1) fp32 output, differentiable in the
+        parameters (models.py:388-394)."""
+        if not coords.is_cuda:
+            raise RuntimeError("SirenWithSnakeTanh.forward runs on the HIP path only (CUDA tensors)")
+        spec = self.hip_spec()
+        lead = coords.shape[:-1]
+        params = [p for _, p in self.named_parameters()]
+        out = _SirenFunction.apply(spec, coords.reshape(-1, spec.in_dim).detach(), *params)
+        return out.reshape(*lead, 1)
+
+
+class _SirenFunction(torch.autograd.Function):
+    """HIP forward/backward of the whole SIREN for an arbitrary upstream gradient."""
+
+    @staticmethod
+    def forward(ctx, spec, coords, *params):
+        from .engine import ROW_TILE, Workspace, cast_shadows, make_net, round_up
+        dev = coords.device
+        lib = _lib.load()
+        L, H = spec.n_inner, spec.hidden
+        n = coords.shape[0]
+        rows = round_up(max(n, 1), ROW_TILE)
+        p = [t.detach().contiguous().float() for t in params]
+        W = [p[2 + 2 * i] for i in range(L)]
+        Wb = [torch.empty(H, H, dtype=torch.bfloat16, device=dev) for _ in range(L)]
+        WTb = [torch.empty(H, H, dtype=torch.bfloat16, device=dev) for _ in range(L)]
+        s = torch.cuda.current_stream(dev).cuda_stream
+        cast_shadows(spec, W, Wb, WTb, s)
+        net = make_net(spec, p[0], p[1], [p[3 + 2 * i] for i in range(L)], Wb, WTb, p[2 + 2 * L],
+                       p[3 + 2 * L])
+        ws = Workspace(spec, rows, dev, train=True)
+        xc = torch.zeros(rows, spec.in_dim, dtype=torch.float32, device=dev)
+        xc[:n] = coords.float()
+        tgt = torch.zeros(rows, dtype=torch.float32, device=dev)
+        b = ws.batch(xc, tgt, n, float(n))
+        _lib.check(lib.siren_forward(ctypes.byref(net), ctypes.byref(b), s), "siren_forward")
+        ctx.keep = (spec, net, ws, xc, tgt, p, Wb, WTb, n, [t.shape for t in params])
+        return ws.out[:n].clone()
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from .engine import SEG_ALIGN, round_up
+        from ._lib import SirenGrads, ptr
+        spec, net, ws, xc, tgt, p, Wb, WTb, n, shapes = ctx.keep
+        lib = _lib.load()
+        dev = xc.device
+        L = spec.n_inner
+        ws.g.zero_()
+        ws.g[:n] = grad_out.reshape(-1).float()
+        offs, off = [], 0
+        for shp in shapes:
+            offs.append(off)
+            off = round_up(off + int(np.prod(shp)), SEG_ALIGN)
+        flat = torch.zeros(off + SEG_ALIGN, dtype=torch.float32, device=dev)
+        views = [flat[o:o + int(np.prod(shp))].view(shp) for o, shp in zip(offs, shapes)]
+        gs = SirenGrads()
+        gs.W0, gs.b0 = ptr(views[0]), ptr(views[1])
+        for i in range(L):
+            gs.W[i], gs.b[i] = ptr(views[2 + 2 * i]), ptr(views[3 + 2 * i])
+        gs.w_head, gs.b_head = ptr(views[2 + 2 * L]), ptr(views[3 + 2 * L])
+        gs.sse, gs.flat, gs.flat_len = flat.data_ptr() + 4 * off, ptr(flat), off + SEG_ALIGN
+        b = ws.batch(xc, tgt, n, float(n))
+        s = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(lib.siren_backward(ctypes.byref(net), ctypes.byref(gs), ctypes.byref(b), s),
+                   "siren_backward")
+        ctx.keep = None
+        return (None, None, *views)

@@ -1,0 +1,160 @@
+"""``train()`` with the reference's keyword API (run.py:30-400) on the HIP engine.
+
+Differences from the reference are limited to what the hot-path scope excludes: no plots
+(matplotlib figures), no loss-landscape, no STFT/MAE/SNR loss mixes (alpha must be 0 and
+loss_mode 'mse' -- at alpha=0 the reference's STFT term contributes exactly zero, SURVEY
+§8 a8), no random-Fourier-feature encoding, no KAN, no MDCT target yet.
+Everything the path produces -- output.wav, the checkpoint dict, parameters.json with the
+run.py-formula SNR -- keeps the reference's names and formats.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import numpy as np
+import scipy.io.wavfile as wavfile
+import torch
+
+from .engine import SirenEngine
+from .models import SirenWithSnakeTanh
+from .utils import WaveformFitting, calculate_snr, get_coord, load_mono_like_librosa, reported_snr
+
+
+def save_parameters(experiment_folder, **kwargs):
+    """run.py:25-28."""
+    with open(f"{experiment_folder}/parameters.json", "w") as file:
+        json.dump(kwargs, file, indent=4)
+
+
+def _rank0() -> bool:
+    d = torch.distributed
+    return not (d.is_available() and d.is_initialized()) or d.get_rank() == 0
+
+
+def train(experiment_path: str, tag: str, inst: str, duration: int, num_channels=1, method='wave',
+          arch='mlp', loss_mode='mse', mode=None, decimation=1, bwe=False, num_hidden_features=256,
+          num_sine=2, num_snake=2, num_tanh=0, num_freq=None, omega=22000, first_linear=False,
+          last_linear=True, hidden_omega=30, a_initial=0.5, total_steps=20000, learning_rate=1e-3,
+          min_learning_rate=1e-6, alpha=0.0, prev_ckpt_path=None, visualization=False, *,
+          filename=None, data_dir="data", seed=None, micro_batch=1 << 20, use_graph=True,
+          device=None, verbose=False):
+    """Fit one clip; returns the checkpoint path (run.py:400).  Extra keyword-only knobs:
+    ``filename`` (default ``{data_dir}/{inst}.wav`` as run.py:33), ``seed`` (torch.manual_seed
+    before model construction), ``micro_batch`` (rows per fused micro-batch), ``use_graph``
+    (replay each step as a HIP graph), ``device``."""
+    if method != "wave":
+        raise NotImplementedError("method='mdct' is SURVEY §8 f2 (not on the HIP path yet)")
+    if arch != "mlp":
+        raise NotImplementedError("arch='kan' is SURVEY §8 f4 (not on the HIP path yet)")
+    if loss_mode != "mse" or alpha != 0.0:
+        raise NotImplementedError("HIP path implements loss_mode='mse' with alpha=0 (run.py:167-169)")
+    if num_freq is not None:
+        raise NotImplementedError("random Fourier features (rff) are out of scope")
+    if visualization:
+        raise NotImplementedError("loss-landscape visualization is out of scope")
+
+    filename = filename or f"{data_dir}/{inst}.wav"
+    experiment_folder = f"{experiment_path}/{inst}-{method}-{tag}"
+    rank0 = _rank0()
+    if rank0:
+        while os.path.exists(experiment_folder):  # run.py:36-38
+            tag = tag + "(2)"
+            experiment_folder = f"{experiment_path}/{inst}-{method}-{tag}"
+        os.makedirs(experiment_folder)
+    decimation = int(decimation)
+
+    input_data = WaveformFitting(filename, duration=duration, decimation=decimation)
+    model_input, ground_truth = input_data[0]
+    input_dimension = 1
+
+    if seed is not None:
+        torch.manual_seed(seed)
+    model = SirenWithSnakeTanh(in_features=input_dimension, out_features=1,
+                               hidden_features=num_hidden_features, num_sine=num_sine,
+                               num_snake=num_snake, num_tanh=num_tanh, num_freq=num_freq,
+                               first_linear=first_linear, last_linear=last_linear,
+                               first_omega_0=omega, hidden_omega_0=hidden_omega, a_initial=a_initial)
+    ckpt = None
+    if prev_ckpt_path is not None:  # run.py:84-106
+        ckpt = torch.load(prev_ckpt_path, map_location="cpu", weights_only=True)
+        model.load_state_dict(ckpt["model_state_dict"])
+
+    dev = torch.device(device or "cuda")
+    engine = SirenEngine(model, model_input, ground_truth, lr=learning_rate, min_lr=min_learning_rate,
+                         micro_batch=micro_batch, hist_cap=total_steps, device=dev)
+    if ckpt is not None:
+        engine.load_adam_state_dict(ckpt["optimizer_state_dict"])
+
+    torch.cuda.synchronize(dev)
+    start_time = time.time()
+    single = not (torch.distributed.is_available() and torch.distributed.is_initialized())
+    if use_graph and single and total_steps > 1:
+        engine.step()                    # step 0 eagerly (also warms up the kernels)
+        engine.capture_graph()
+        for _ in range(total_steps - 1):
+            engine.step()
+    else:
+        for _ in range(total_steps):
+            engine.step()
+    torch.cuda.synchronize(dev)
+    end_time = time.time()
+    total_time = (end_time - start_time) / 60
+
+    raw_losses, raw_lrs = engine.history()
+    losses = 10 * np.log10(raw_losses.astype(np.float64) + 1e-10)   # run.py:180
+    lrs = 10 * np.log10(raw_lrs)                                     # run.py:190
+    best_iter = int(np.argmin(raw_losses)) if len(raw_losses) else -1
+
+    param_size = sum(p.nelement() * p.element_size() for p in model.parameters())
+    buffer_size = sum(b.nelement() * b.element_size() for b in model.buffers())
+    model_size = (param_size + buffer_size) / 1024
+
+    # inference (run.py:251-256); best_model aliases the final model (run.py:173)
+    if bwe:
+        coords = get_coord(input_data.original_sample_rate * duration, dim=1)
+        recover_sample_rate = input_data.original_sample_rate
+    else:
+        coords = model_input
+        recover_sample_rate = input_data.sample_rate
+    signal_recovered = engine.infer(coords.to(dev)).cpu().numpy().astype(np.float32)
+
+    ckpt_path = f"{experiment_folder}/saved_ckpt.pt"
+    if rank0:
+        output_filename = f"{experiment_folder}/output.wav"
+        wavfile.write(output_filename, recover_sample_rate, signal_recovered.reshape(-1, 1))
+        ref, fs_ref = load_mono_like_librosa(filename)
+        rec, _ = load_mono_like_librosa(output_filename)
+        snr_final = float(reported_snr(ref, fs_ref, rec, duration, decimation, bwe))
+        target = ground_truth.numpy().reshape(-1)
+        snr_target = float(calculate_snr(target, signal_recovered)) if not bwe else None
+
+        checkpoint = {"model_state_dict": {k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
+                      "optimizer_state_dict": engine.adam_state_dict()}
+        torch.save(checkpoint, ckpt_path)
+
+        n_gpus = torch.distributed.get_world_size() if not single else 1
+        params = {
+            "experiment_path": experiment_path, "tag": tag, "inst": inst, "duration": duration,
+            "num_channels": num_channels, "method": method, "arch": arch, "loss_mode": loss_mode,
+            "mode": mode, "decimation": decimation, "bwe": bwe,
+            "num_hidden_features": num_hidden_features, "num_sine": num_sine,
+            "num_snake": num_snake, "num_tanh": num_tanh, "num_freq": num_freq, "omega": omega,
+            "hidden_omega": hidden_omega, "a_initial": a_initial, "total_steps": total_steps,
+            "learning_rate": learning_rate, "min_learning_rate": min_learning_rate, "alpha": alpha,
+            "prev_ckpt_path": prev_ckpt_path, "curr_ckpt_path": ckpt_path,
+            "visualization": visualization, "parameter_size(KB)": param_size / 1024,
+            "total_model_size(KB)": model_size, "total_trainig_time(min)": total_time,
+            "SNR": snr_final,
+            # additions of this build
+            "SNR_target": snr_target, "best_iter": best_iter,
+            "final_loss": float(raw_losses[-1]) if len(raw_losses) else None,
+            "coord_samples_per_sec": engine.n_total * total_steps / max(total_time * 60, 1e-9),
+            "n_gpus": n_gpus,
+        }
+        save_parameters(experiment_folder, **params)
+        if verbose:
+            print(json.dumps({"SNR": snr_final, "SNR_target": snr_target, "time_min": total_time}))
+    train.last_history = (losses, lrs)
+    return ckpt_path

@@ -1,0 +1,12 @@
+"""Import shim: the package lives in the directory ``inr-for-audio_amd/`` (a name Python
+cannot import directly).  ``import inr_for_audio_amd`` loads that directory as a package."""
+import importlib.util as _ilu
+import os as _os
+import sys as _sys
+
+_DIR = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "inr-for-audio_amd")
+_spec = _ilu.spec_from_file_location(__name__, _os.path.join(_DIR, "__init__.py"),
+                                     submodule_search_locations=[_DIR])
+_mod = _ilu.module_from_spec(_spec)
+_sys.modules[__name__] = _mod
+_spec.loader.exec_module(_mod)

@@ -1,0 +1,268 @@
+"""CPU ORACLE for the SIREN hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module, and only as the checker / the timed CPU baseline.  The product package
+(inr-for-audio_amd/) never imports it.
+
+A numpy restatement of the reference algorithm (senyuanfan/inr-for-audio):
+  * get_coord / torch.linspace                utils.py:99-109
+  * WaveformFitting target normalisation      utils.py:111-149
+  * SineLayer / SirenWithSnakeTanh forward    models.py:114-115, 388-394 (sine-only)
+  * MSELoss + autograd backward               run.py:125,168,185
+  * torch.optim.Adam step                     run.py:116,186
+  * ReduceLROnPlateau(min, 0.8, 200)          run.py:117,187
+  * calculate_snr + run.py's reported SNR     utils.py:77-97, run.py:302-335
+
+Pinned against golden vectors generated from the reference itself (tests/golden/,
+made by tests/golden/make_golden.py, which imports /root/reference in the build
+container); see tests/test_oracle.py.
+
+Precision model: `dtype=np.float64` gives the exact-arithmetic answer; `bf16=True`
+rounds exactly the tensors the HIP path stores in bf16 (hidden weights, Y_i = sin,
+C_i = cos, dZ_i) so the GPU can be checked tightly against it.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+from scipy.signal import decimate
+
+F32 = np.float32
+F64 = np.float64
+
+
+# ------------------------------------------------------------------ numerics helpers
+def bf16_round(x: np.ndarray) -> np.ndarray:
+    """Round-to-nearest-even to bf16, returned as float32 (v_cvt_pk_bf16_f32 semantics)."""
+    x = np.ascontiguousarray(x, dtype=F32)
+    u = x.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    out = r.astype(np.uint32).view(F32).copy()
+    nan = np.isnan(x)
+    out[nan] = x[nan]
+    return out
+
+
+def fma32(a, b, c) -> np.ndarray:
+    """fp32 fused multiply-add: a*b is exact in fp64, one rounding of the sum to fp32
+    (double rounding through fp64 differs from a true fma in < 2^-29 of cases)."""
+    return (np.asarray(a, F64) * np.asarray(b, F64) + np.asarray(c, F64)).astype(F32)
+
+
+# ------------------------------------------------------------------ data (utils.py)
+def linspace_f32(n: int, start: float = -1.0, end: float = 1.0) -> np.ndarray:
+    """torch.linspace scalar formula (fp32): i < n/2: start + step*i; else end - step*(n-1-i)."""
+    if n == 1:
+        return np.array([start], F32)
+    step = F32((F32(end) - F32(start)) / F32(n - 1))
+    i = np.arange(n, dtype=np.int64)
+    half = n // 2
+    lo = (F32(start) + step * i[:half].astype(F32)).astype(F32)
+    hi = (F32(end) - step * (n - 1 - i[half:]).astype(F32)).astype(F32)
+    return np.concatenate([lo, hi]).astype(F32)
+
+
+def waveform_target(data: np.ndarray, duration: int, sample_rate: int, decimation: int = 1):
+    """WaveformFitting (utils.py:111-149): trim, optional decimate, peak-normalise."""
+    x = np.asarray(data).astype(F32)[0:duration * sample_rate]
+    if decimation > 1:
+        x = decimate(x, q=int(decimation))
+    return (x / np.max(np.abs(x))).astype(F32)
+
+
+# ------------------------------------------------------------------ model (models.py)
+class Params:
+    """SIREN parameters in nn.Linear layout: W0 [H,in], b0 [H], W[i] [H,H], b[i] [H],
+    wf [H] (= net.{L+1}.weight[0]), bf scalar."""
+
+    def __init__(self, W0, b0, W, b, wf, bf):
+        self.W0, self.b0 = np.asarray(W0, F32), np.asarray(b0, F32)
+        self.W = [np.asarray(w, F32) for w in W]
+        self.b = [np.asarray(x, F32) for x in b]
+        self.wf = np.asarray(wf, F32).reshape(-1)
+        self.bf = F32(np.asarray(bf).reshape(-1)[0])
+
+    @classmethod
+    def from_state_dict(cls, sd: dict, n_inner: int):
+        g = lambda k: np.asarray(sd[k], F32)  # noqa: E731
+        return cls(g("net.0.linear.weight"), g("net.0.linear.bias"),
+                   [g(f"net.{i}.linear.weight") for i in range(1, n_inner + 1)],
+                   [g(f"net.{i}.linear.bias") for i in range(1, n_inner + 1)],
+                   g(f"net.{n_inner + 1}.weight"), g(f"net.{n_inner + 1}.bias"))
+
+    def to_state_dict(self) -> dict:
+        L = len(self.W)
+        sd = {"net.0.linear.weight": self.W0, "net.0.linear.bias": self.b0}
+        for i in range(L):
+            sd[f"net.{i + 1}.linear.weight"] = self.W[i]
+            sd[f"net.{i + 1}.linear.bias"] = self.b[i]
+        sd[f"net.{L + 1}.weight"] = self.wf.reshape(1, -1)
+        sd[f"net.{L + 1}.bias"] = np.array([self.bf], F32)
+        return sd
+
+    def flat(self) -> list[np.ndarray]:
+        return [self.W0, self.b0] + [x for pair in zip(self.W, self.b) for x in pair] + \
+               [self.wf.reshape(1, -1), np.array([self.bf], F32)]
+
+
+def first_preact(t: np.ndarray, W0: np.ndarray, b0: np.ndarray, omega0: float) -> np.ndarray:
+    """omega0 * (t W0^T + b0) in fp32 with torch-CPU addmm rounding (K=1: fma(t,w,b);
+    K=2: fma(t1,w1,t0*w0)+b) then the fp32 multiply."""
+    t = np.asarray(t, F32).reshape(t.shape[0], -1)
+    if t.shape[1] == 1:
+        z = fma32(t[:, :1], W0[None, :, 0], b0[None, :])
+    else:
+        p = (t[:, :1] * W0[None, :, 0]).astype(F32)
+        z = (fma32(t[:, 1:2], W0[None, :, 1], p) + b0[None, :]).astype(F32)
+    return (F32(omega0) * z).astype(F32)
+
+
+def sin32(a: np.ndarray) -> np.ndarray:
+    return np.sin(np.asarray(a, F64)).astype(F32)
+
+
+def cos32(a: np.ndarray) -> np.ndarray:
+    return np.cos(np.asarray(a, F64)).astype(F32)
+
+
+def forward(p: Params, t: np.ndarray, omega0: float, omega: float, bf16: bool = False,
+            dtype=F32):
+    """Returns (out [N], cache).  cache: Y[0..L] (layer outputs), A[0..L] (omega*linear),
+    C[1..L] cos of inner pre-activations; bf16-rounded where the HIP path stores bf16."""
+    A0 = first_preact(t, p.W0, p.b0, omega0)
+    Y0 = sin32(A0)
+    Y = [bf16_round(Y0) if bf16 else Y0]
+    A, C = [A0], [None]
+    for Wi, bi in zip(p.W, p.b):
+        Wm = bf16_round(Wi) if bf16 else Wi
+        z = np.asarray(Y[-1], dtype) @ np.asarray(Wm, dtype).T + np.asarray(bi, dtype)
+        a = (F64(omega) * np.asarray(z, F64)) if dtype == F64 else (F32(omega) * z.astype(F32))
+        y, c = np.sin(a), np.cos(a)
+        if bf16:
+            y, c = bf16_round(y), bf16_round(c)
+        A.append(a)
+        Y.append(np.asarray(y, dtype if not bf16 else F32))
+        C.append(np.asarray(c, dtype if not bf16 else F32))
+    out = np.asarray(Y[-1], dtype) @ np.asarray(p.wf, dtype) + dtype(p.bf)
+    return out, {"Y": Y, "A": A, "C": C}
+
+
+def mse(out: np.ndarray, y: np.ndarray) -> float:
+    d = np.asarray(out, F64) - np.asarray(y, F64).reshape(-1)
+    return float(np.mean(d * d))
+
+
+def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float, omega: float,
+             bf16: bool = False, dtype=F64) -> dict:
+    """Autograd of the SIREN for upstream dLoss/dout = g [N].  Returns a dict of grads in
+    nn.Linear layout (same keys as Params.to_state_dict)."""
+    L = len(p.W)
+    Y, A, C = cache["Y"], cache["A"], cache["C"]
+    g = np.asarray(g, dtype).reshape(-1)
+    grads = {}
+    grads[f"net.{L + 1}.weight"] = (g @ np.asarray(Y[L], dtype)).reshape(1, -1)
+    grads[f"net.{L + 1}.bias"] = np.array([g.sum()])
+    dY = g[:, None] * np.asarray(p.wf, dtype)[None, :]
+    for i in range(L, 0, -1):
+        cos_i = np.asarray(C[i], dtype) if bf16 else np.cos(np.asarray(A[i], F64)).astype(dtype)
+        dZ = dY * cos_i * dtype(omega)
+        if bf16:
+            db = dZ.sum(0)
+            dZ = bf16_round(dZ).astype(dtype)
+        else:
+            db = dZ.sum(0)
+        grads[f"net.{i}.linear.weight"] = dZ.T @ np.asarray(Y[i - 1], dtype)
+        grads[f"net.{i}.linear.bias"] = db
+        Wm = bf16_round(p.W[i - 1]) if bf16 else p.W[i - 1]
+        dY = dZ @ np.asarray(Wm, dtype)
+    cos0 = np.cos(np.asarray(A[0], F64)).astype(dtype)
+    dZ0 = dY * cos0 * dtype(omega0)
+    tt = np.asarray(t, dtype).reshape(dZ0.shape[0], -1)
+    grads["net.0.linear.weight"] = dZ0.T @ tt
+    grads["net.0.linear.bias"] = dZ0.sum(0)
+    return grads
+
+
+def mse_grad(out: np.ndarray, y: np.ndarray, n_total: int | None = None) -> np.ndarray:
+    """MSELoss(mean) backward: (out - y) * (2/N) in fp32 (torch's norm scalar)."""
+    n = out.shape[0] if n_total is None else n_total
+    return ((np.asarray(out, F32) - np.asarray(y, F32).reshape(-1)) * F32(2.0 / n)).astype(F32)
+
+
+# ------------------------------------------------------------------ optimizer (run.py)
+def adam_step(param, grad, exp_avg, exp_avg_sq, step: int, lr: float, beta1=0.9, beta2=0.999,
+              eps=1e-8):
+    """torch.optim.Adam (CUDA rounding sequence, see elementwise.hip adam_flat_kernel).
+    `step` is the 1-based step count after increment.  Returns new (p, m, v) fp32."""
+    p, g = np.asarray(param, F32), np.asarray(grad, F32)
+    m, v = np.asarray(exp_avg, F32), np.asarray(exp_avg_sq, F32)
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    neg_step = F32((lr / bc1) * -1.0)
+    bc2_sqrt = F32(math.sqrt(bc2))
+    m = fma32(F32(1.0 - beta1), (g - m).astype(F32), m)
+    v = fma32((F32(1.0 - beta2) * g).astype(F32), g, (v * F32(beta2)).astype(F32))
+    d = ((np.sqrt(v).astype(F32) / bc2_sqrt).astype(F32) + F32(eps)).astype(F32)
+    p = (p + ((neg_step * m).astype(F32) / d).astype(F32)).astype(F32)
+    return p, m, v
+
+
+class Plateau:
+    """torch.optim.lr_scheduler.ReduceLROnPlateau(mode='min', factor, patience,
+    threshold=1e-4 (rel), cooldown=0, min_lr, eps=1e-8)."""
+
+    def __init__(self, lr, factor=0.8, patience=200, min_lr=1e-6, threshold=1e-4, eps=1e-8):
+        self.lr, self.factor, self.patience, self.min_lr = lr, factor, patience, min_lr
+        self.threshold, self.eps = threshold, eps
+        self.best, self.num_bad, self.last_epoch = math.inf, 0, 0
+
+    def step(self, loss: float) -> float:
+        cur = float(loss)
+        self.last_epoch += 1
+        if cur < self.best * (1.0 - self.threshold):
+            self.best, self.num_bad = cur, 0
+        else:
+            self.num_bad += 1
+        if self.num_bad > self.patience:
+            new_lr = max(self.lr * self.factor, self.min_lr)
+            if self.lr - new_lr > self.eps:
+                self.lr = new_lr
+            self.num_bad = 0
+        return self.lr
+
+
+# ------------------------------------------------------------------ metrics (utils.py / run.py)
+def calculate_snr(ref, rec) -> float:
+    ref, rec = np.asarray(ref), np.asarray(rec)
+    return float(10 * np.log10(np.mean(ref ** 2) / np.mean((rec - ref) ** 2)))
+
+
+def reported_snr(ref_raw, fs, rec, duration, decimation=1) -> float:
+    """run.py:306-335: trim, decimate(q) (a low-pass even at q=1), +1e-10, SNR."""
+    ref = np.asarray(ref_raw)[:int(fs * duration)]
+    ref = decimate(ref, q=int(decimation)) + 1e-10
+    return calculate_snr(ref, rec)
+
+
+# ------------------------------------------------------------------ full-batch fit (run.py:156-190)
+def fit(p: Params, t, y, omega0, omega, steps, lr=1e-3, min_lr=1e-6, bf16=False):
+    """Full-batch fit with the restated loop; returns (params, losses, lrs)."""
+    names = list(p.to_state_dict().keys())
+    flat = [x.astype(F32).copy() for x in p.to_state_dict().values()]
+    ms = [np.zeros_like(x) for x in flat]
+    vs = [np.zeros_like(x) for x in flat]
+    sched = Plateau(lr, min_lr=min_lr)
+    losses, lrs = [], []
+    L = len(p.W)
+    for k in range(1, steps + 1):
+        cur = Params.from_state_dict(dict(zip(names, flat)), L)
+        out, cache = forward(cur, t, omega0, omega, bf16=bf16)
+        loss = F32(mse(out, y))
+        grads = backward(cur, t, cache, mse_grad(out, y), omega0, omega, bf16=bf16)
+        for j, nme in enumerate(names):
+            flat[j], ms[j], vs[j] = adam_step(flat[j], grads[nme].astype(F32).reshape(flat[j].shape),
+                                              ms[j], vs[j], k, sched.lr)
+        losses.append(float(loss))
+        lrs.append(sched.step(loss))
+    return Params.from_state_dict(dict(zip(names, flat)), L), np.array(losses), np.array(lrs)

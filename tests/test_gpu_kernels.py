@@ -1,0 +1,289 @@
+"""Per-kernel parity of libsiren_hip.so against the CPU oracle (called through the C-ABI).
+
+Tolerances: bf16-stored outputs (Y = sin, C = cos, dZ) must be within one bf16 rounding of
+the fp64 answer computed from the same bf16 inputs (|err| <= 2^-8 |x| + small fp32
+accumulation slack); fp32 reductions within 1e-5 relative; Adam and the coordinate grid
+bit-exact.
+"""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import siren_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+F32 = np.float32
+
+
+def ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def S():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ok(status, lib):
+    assert status == 0, lib.siren_status_string(status)
+
+
+def to_dev(a, dev, dtype=torch.float32):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=F32)).to(dev).to(dtype)
+
+
+def bf16_np(t: torch.Tensor) -> np.ndarray:
+    return t.float().cpu().numpy()
+
+
+def within_bf16(got, ref, abs_slack=1e-5):
+    """|got - ref| <= 2^-8 * |ref| + abs_slack elementwise (one bf16 rounding + slack)."""
+    err = np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64))
+    bound = np.abs(np.asarray(ref, np.float64)) * 2.0 ** -8 + abs_slack
+    return float(np.max(err - bound))
+
+
+@pytest.mark.parametrize("n,rows,offset", [(1, 128, 0), (7, 128, 0), (44100, 44160, 0),
+                                          (1 << 20, 1 << 20, 0), (441000, 1024, 220000),
+                                          (441000, 1024, 440500)])
+def test_coords_fill_bit_exact(lib, dev, n, rows, offset):
+    t = torch.full((rows,), float("nan"), device=dev)
+    ok(lib.siren_coords_fill(ptr(t), rows, offset, n, S()), lib)
+    got = t.cpu().numpy()
+    ref_full = orc.linspace_f32(n)
+    valid = max(0, min(rows, n - offset))
+    assert np.array_equal(got[:valid], ref_full[offset:offset + valid])
+    assert np.all(got[valid:] == 0)
+
+
+@pytest.mark.parametrize("in_dim", [1, 2])
+@pytest.mark.parametrize("omega0", [30.0, 1000.0, 22000.0])
+def test_first_fwd(lib, dev, in_dim, omega0):
+    rng = np.random.default_rng(1)
+    R, H = 1024, 256
+    t = rng.uniform(-1, 1, (R, in_dim)).astype(F32)
+    W0 = rng.uniform(-1, 1, (H, in_dim)).astype(F32)
+    b0 = rng.uniform(-1, 1, H).astype(F32)
+    Y0 = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    ok(lib.siren_first_fwd(ptr(to_dev(t, dev)), in_dim, ptr(to_dev(W0, dev)), ptr(to_dev(b0, dev)),
+                           ctypes.c_float(omega0), R, H, ptr(Y0), S()), lib)
+    ref = orc.sin32(orc.first_preact(t, W0, b0, omega0))  # fp32 restatement, correctly rounded sin
+    got = bf16_np(Y0)
+    assert within_bf16(got, ref, abs_slack=1e-6) <= 0
+    assert np.mean(got == orc.bf16_round(ref)) > 0.995
+
+
+def _inner_inputs(rng, R, H):
+    X = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    lim = math.sqrt(6 / H) / 30
+    W = rng.uniform(-lim, lim, (H, H)).astype(F32)
+    b = rng.uniform(-1 / math.sqrt(H), 1 / math.sqrt(H), H).astype(F32)
+    return X, W, b
+
+
+@pytest.mark.parametrize("R,H", [(256, 128), (512, 256), (384, 512), (256, 1024)])
+@pytest.mark.parametrize("head", [False, True])
+def test_inner_fwd(lib, dev, R, H, head):
+    rng = np.random.default_rng(2)
+    X, W, b = _inner_inputs(rng, R, H)
+    Wb = orc.bf16_round(W)
+    hw = rng.uniform(-0.01, 0.01, H).astype(F32)
+    Y = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    C = torch.empty_like(Y)
+    hp = torch.zeros(H // 128, R, device=dev)
+    ok(lib.siren_inner_fwd(ptr(to_dev(X, dev, torch.bfloat16)), ptr(to_dev(Wb, dev, torch.bfloat16)),
+                           ptr(to_dev(b, dev)), ctypes.c_float(30.0), R, H, ptr(Y), ptr(C),
+                           ptr(to_dev(hw, dev)) if head else None, ptr(hp) if head else None, S()), lib)
+    a = 30.0 * (X.astype(np.float64) @ Wb.astype(np.float64).T + b)
+    assert within_bf16(bf16_np(Y), np.sin(a), 2e-5) <= 0
+    assert within_bf16(bf16_np(C), np.cos(a), 2e-5) <= 0
+    if head:
+        ref = np.sin(a) @ hw.astype(np.float64)
+        got = hp.cpu().numpy().astype(np.float64).sum(0)
+        assert np.max(np.abs(got - ref)) < 1e-4 * max(1.0, np.max(np.abs(ref)))
+
+
+def test_head_loss(lib, dev):
+    rng = np.random.default_rng(3)
+    R, nparts, n_valid, n_total = 1024, 4, 1000, 5000
+    hp = rng.normal(size=(nparts, R)).astype(F32)
+    y = rng.normal(size=R).astype(F32)
+    bh = np.array([0.25], F32)
+    out = torch.empty(R, device=dev)
+    g = torch.empty(R, device=dev)
+    sse = torch.empty((R + 255) // 256, device=dev)
+    gs = torch.empty_like(sse)
+    ok(lib.siren_head_loss(ptr(to_dev(hp, dev)), nparts, R, ptr(to_dev(bh, dev)), ptr(to_dev(y, dev)),
+                           n_valid, ctypes.c_double(n_total), ptr(out), ptr(g), ptr(sse), ptr(gs), S()),
+       lib)
+    o_ref = hp.astype(np.float64).sum(0) + 0.25
+    assert np.allclose(out.cpu().numpy(), o_ref, atol=1e-5)
+    g_ref = np.where(np.arange(R) < n_valid, (o_ref - y) * (2.0 / n_total), 0.0)
+    assert np.allclose(g.cpu().numpy(), g_ref, rtol=1e-5, atol=1e-9)
+    assert abs(sse.cpu().numpy().astype(np.float64).sum() - np.sum((o_ref - y)[:n_valid] ** 2)) < 1e-3
+    assert abs(gs.cpu().numpy().astype(np.float64).sum() - g_ref.sum()) < 1e-6
+
+
+@pytest.mark.parametrize("H", [128, 256, 1024])
+def test_head_bwd(lib, dev, H):
+    rng = np.random.default_rng(4)
+    R = 512
+    C = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    Y = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    g = rng.normal(size=R).astype(F32) * 1e-3
+    w = rng.uniform(-0.01, 0.01, H).astype(F32)
+    dZ = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    dbp = torch.empty(R // 128, H, device=dev)
+    dwp = torch.empty(R // 128, H, device=dev)
+    ok(lib.siren_head_bwd(ptr(to_dev(C, dev, torch.bfloat16)), ptr(to_dev(Y, dev, torch.bfloat16)),
+                          ptr(to_dev(g, dev)), ptr(to_dev(w, dev)), ctypes.c_float(30.0), R, H, ptr(dZ),
+                          ptr(dbp), ptr(dwp), S()), lib)
+    dz_ref = g[:, None].astype(np.float64) * w[None, :] * C * 30.0
+    assert within_bf16(bf16_np(dZ), dz_ref, 1e-12) <= 0
+    assert np.allclose(dbp.cpu().numpy().astype(np.float64).sum(0), dz_ref.sum(0), rtol=1e-4, atol=1e-9)
+    assert np.allclose(dwp.cpu().numpy().astype(np.float64).sum(0), (g[:, None] * Y).sum(0), rtol=1e-4,
+                       atol=1e-9)
+
+
+@pytest.mark.parametrize("R,H", [(256, 128), (512, 256), (256, 1024)])
+def test_inner_bwd_dx(lib, dev, R, H):
+    rng = np.random.default_rng(5)
+    dZ = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
+    _, W, _ = _inner_inputs(rng, R, H)
+    Wb = orc.bf16_round(W)
+    Cp = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    out = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    dbp = torch.empty(R // 128, H, device=dev)
+    WT = np.ascontiguousarray(Wb.T)
+    ok(lib.siren_inner_bwd_dx(ptr(to_dev(dZ, dev, torch.bfloat16)), ptr(to_dev(WT, dev, torch.bfloat16)),
+                              ptr(to_dev(Cp, dev, torch.bfloat16)), ctypes.c_float(30.0), R, H, ptr(out),
+                              ptr(dbp), S()), lib)
+    ref = (dZ.astype(np.float64) @ Wb.astype(np.float64)) * Cp * 30.0
+    scale = np.max(np.abs(ref))
+    assert within_bf16(bf16_np(out), ref, 1e-5 * scale) <= 0
+    db = dbp.cpu().numpy().astype(np.float64).sum(0)
+    assert np.max(np.abs(db - ref.sum(0))) < 1e-4 * np.max(np.abs(ref.sum(0))) + 1e-6 * scale
+
+
+@pytest.mark.parametrize("in_dim", [1, 2])
+@pytest.mark.parametrize("omega0", [1000.0, 22000.0])
+def test_first_bwd_dx(lib, dev, in_dim, omega0):
+    rng = np.random.default_rng(6)
+    R, H = 512, 256
+    dZ1 = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
+    _, W, _ = _inner_inputs(rng, R, H)
+    Wb = orc.bf16_round(W)
+    t = rng.uniform(-1, 1, (R, in_dim)).astype(F32)
+    W0 = rng.uniform(-1 / in_dim, 1 / in_dim, (H, in_dim)).astype(F32)
+    b0 = rng.uniform(-1, 1, H).astype(F32)
+    part = torch.empty(R // 128, 1 + in_dim, H, device=dev)
+    WT = np.ascontiguousarray(Wb.T)
+    ok(lib.siren_first_bwd_dx(ptr(to_dev(dZ1, dev, torch.bfloat16)), ptr(to_dev(WT, dev, torch.bfloat16)),
+                              ptr(to_dev(t, dev)), in_dim, ptr(to_dev(W0, dev)), ptr(to_dev(b0, dev)),
+                              ctypes.c_float(omega0), R, H, ptr(part), S()), lib)
+    A0 = orc.first_preact(t, W0, b0, omega0)
+    dz0 = (dZ1.astype(np.float64) @ Wb.astype(np.float64)) * np.cos(A0.astype(np.float64)) * omega0
+    got = part.cpu().numpy().astype(np.float64).sum(0)
+    ref_db = dz0.sum(0)
+    scale = np.max(np.abs(dz0)) * math.sqrt(R)
+    assert np.max(np.abs(got[0] - ref_db)) < 1e-4 * scale
+    for j in range(in_dim):
+        ref_w = (dz0 * t[:, j:j + 1]).sum(0)
+        assert np.max(np.abs(got[1 + j] - ref_w)) < 1e-4 * scale
+
+
+@pytest.mark.parametrize("R,H,splits", [(256, 128, 1), (1024, 256, 3), (2048, 256, 16),
+                                        (512, 1024, 2), (640, 512, 5)])
+def test_inner_bwd_dw(lib, dev, R, H, splits):
+    rng = np.random.default_rng(7)
+    Y = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    dZ = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
+    slab = torch.empty(int(lib.siren_slab_floats(H, splits)), device=dev)
+    grad = torch.full((H, H), 0.5, device=dev)
+    ok(lib.siren_inner_bwd_dw(ptr(to_dev(Y, dev, torch.bfloat16)), ptr(to_dev(dZ, dev, torch.bfloat16)),
+                              R, H, splits, ptr(slab), S()), lib)
+    ok(lib.siren_dw_reduce(ptr(slab), splits, H, ptr(grad), 1, S()), lib)
+    ref = dZ.astype(np.float64).T @ Y.astype(np.float64) + 0.5
+    got = grad.cpu().numpy().astype(np.float64)
+    assert np.max(np.abs(got - ref)) < 1e-5 * np.max(np.abs(ref - 0.5)) + 1e-7
+
+
+def test_col_reduce(lib, dev):
+    rng = np.random.default_rng(8)
+    for nrows, ncols, stride in [(3, 70, 1), (300, 256, 1), (8192, 1024, 2)]:
+        part = rng.normal(size=(nrows, ncols)).astype(F32)
+        out = torch.full((ncols * stride,), 1.0, device=dev)
+        tmp = torch.empty(64, ncols, device=dev)
+        ok(lib.siren_col_reduce(ptr(to_dev(part, dev)), ncols, nrows, ncols, ptr(out), stride, 1, ptr(tmp),
+                                S()), lib)
+        got = out.cpu().numpy()[::stride]
+        assert np.allclose(got, part.astype(np.float64).sum(0) + 1.0, rtol=1e-5, atol=1e-4)
+
+
+def _state_tensor(dev, **kw):
+    from inr_for_audio_amd._lib import SirenOptState
+    st = SirenOptState()
+    st.lr, st.best, st.step = kw.get("lr", 1e-3), math.inf, kw.get("step", 0.0)
+    st.min_lr, st.factor, st.threshold, st.eps_lr = kw.get("min_lr", 1e-6), 0.8, 1e-4, 1e-8
+    st.patience = kw.get("patience", 200)
+    st.beta1, st.beta2, st.eps = 0.9, 0.999, 1e-8
+    return torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(dev)
+
+
+def _read_state(t):
+    from inr_for_audio_amd._lib import SirenOptState
+    return SirenOptState.from_buffer_copy(bytes(t.cpu().numpy().tobytes()))
+
+
+def test_adam_bit_exact(lib, dev):
+    rng = np.random.default_rng(9)
+    n = 100003
+    p = (rng.normal(size=n) * 0.05).astype(F32)
+    m = np.zeros(n, F32)
+    v = np.zeros(n, F32)
+    pd, md, vd = to_dev(p, dev), to_dev(m, dev), to_dev(v, dev)
+    for step in range(1, 6):
+        g = (rng.normal(size=n) * 10.0 ** rng.uniform(-6, 0, n)).astype(F32)
+        st = _state_tensor(dev, lr=1e-3 * step, step=float(step - 1))
+        ok(lib.siren_adam_step(ptr(pd), ptr(to_dev(g, dev)), ptr(md), ptr(vd), n, ptr(st), S()), lib)
+        p, m, v = orc.adam_step(p, g, m, v, step, 1e-3 * step)
+        assert np.array_equal(md.cpu().numpy(), m)
+        assert np.array_equal(vd.cpu().numpy(), v)
+        assert np.array_equal(pd.cpu().numpy(), p)
+
+
+def test_plateau_trace(lib, dev):
+    rng = np.random.default_rng(10)
+    steps, patience = 400, 20
+    st = _state_tensor(dev, lr=1e-3, patience=patience, min_lr=2e-4)
+    lh = torch.zeros(steps, device=dev)
+    rh = torch.zeros(steps, dtype=torch.float64, device=dev)
+    sse = torch.zeros(1, device=dev)
+    ref = orc.Plateau(1e-3, patience=patience, min_lr=2e-4)
+    losses = np.concatenate([np.linspace(1, 0.5, 100), 0.5 + 0.01 * rng.random(300)]).astype(F32)
+    n_total = 1000.0
+    for k in range(steps):
+        sse.fill_(float(losses[k]) * n_total)
+        ok(lib.siren_plateau_step(ptr(st), ptr(sse), ctypes.c_double(n_total), ptr(lh), ptr(rh), steps, S()),
+           lib)
+        loss32 = float(np.float32(np.float64(np.float32(float(losses[k]) * n_total)) / n_total))
+        ref.step(loss32)
+    got_lr = rh.cpu().numpy()
+    s = _read_state(st)
+    assert s.step == steps and s.last_epoch == steps
+    assert abs(got_lr[-1] - ref.lr) < 1e-15
+    assert s.num_bad == ref.num_bad
+
+
+@pytest.mark.parametrize("H", [128, 1024])
+def test_cast_weight(lib, dev, H):
+    rng = np.random.default_rng(11)
+    W = rng.normal(size=(H, H)).astype(F32)
+    Wb = torch.empty(H, H, dtype=torch.bfloat16, device=dev)
+    WTb = torch.empty_like(Wb)
+    ok(lib.siren_cast_weight(ptr(to_dev(W, dev)), H, H, ptr(Wb), ptr(WTb), S()), lib)
+    assert np.array_equal(bf16_np(Wb), orc.bf16_round(W))
+    assert np.array_equal(bf16_np(WTb), orc.bf16_round(W).T)
