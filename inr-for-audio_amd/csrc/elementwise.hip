@@ -15,7 +15,8 @@ static inline int grid_for(int64_t n, int per_block, int cap = 8192) {
 
 // ---------------------------------------------------------------------------------
 // get_coord / torch.linspace(-1, 1, N) (utils.py:99-109), evaluated at global indices
-// [offset, offset+rows): i < N/2 -> -1 + i*step, else 1 - (N-1-i)*step, step = 2/(N-1).
+// [offset, offset+rows): i < N/2 -> fma(step, i, -1), else fma(-step, N-1-i, 1), step = 2/(N-1)
+// (the contracted form torch's CPU kernel computes; bit-exact with torch.linspace).
 __global__ void coords_fill_kernel(float* t, int64_t rows, int64_t offset, int64_t n_total) {
   const float step = (n_total > 1) ? 2.0f / (float)(n_total - 1) : 0.f;
   const int64_t half = n_total / 2;
@@ -25,8 +26,8 @@ __global__ void coords_fill_kernel(float* t, int64_t rows, int64_t offset, int64
     float v;
     if (i >= n_total) v = 0.f;  // padding rows
     else if (n_total == 1) v = -1.0f;
-    else if (i < half) v = -1.0f + step * (float)i;
-    else v = 1.0f - step * (float)(n_total - 1 - i);
+    else if (i < half) v = __builtin_fmaf(step, (float)i, -1.0f);
+    else v = __builtin_fmaf(-step, (float)(n_total - 1 - i), 1.0f);
     t[r] = v;
   }
 }
@@ -250,7 +251,8 @@ __global__ void adam_flat_kernel(float* __restrict__ p, const float* __restrict_
     float mi = m[i], vi = v[i];
     mi = __builtin_fmaf(w1, gi - mi, mi);
     vi = __builtin_fmaf(w2 * gi, gi, vi * b2);
-    const float d = __fsqrt_rn(vi) / bc2_sqrt + eps;
+    // sqrtf lowers to the correctly rounded sequence (hipcc's __fsqrt_rn is bare v_sqrt_f32)
+    const float d = sqrtf(vi) / bc2_sqrt + eps;
     p[i] = p[i] + (neg_step_size * mi) / d;
     m[i] = mi;
     v[i] = vi;

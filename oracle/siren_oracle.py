@@ -52,14 +52,16 @@ def fma32(a, b, c) -> np.ndarray:
 
 # ------------------------------------------------------------------ data (utils.py)
 def linspace_f32(n: int, start: float = -1.0, end: float = 1.0) -> np.ndarray:
-    """torch.linspace scalar formula (fp32): i < n/2: start + step*i; else end - step*(n-1-i)."""
+    """torch.linspace (fp32, CPU kernel): step = (end-start)/(n-1) in fp32; i < n/2:
+    fma(step, i, start), else fma(-step, n-1-i, end) -- the contracted form torch's CPU
+    build produces (checked bit-exact against torch.linspace in tests/test_oracle.py)."""
     if n == 1:
         return np.array([start], F32)
     step = F32((F32(end) - F32(start)) / F32(n - 1))
     i = np.arange(n, dtype=np.int64)
     half = n // 2
-    lo = (F32(start) + step * i[:half].astype(F32)).astype(F32)
-    hi = (F32(end) - step * (n - 1 - i[half:]).astype(F32)).astype(F32)
+    lo = fma32(step, i[:half].astype(F32), F32(start))
+    hi = fma32(-step, (n - 1 - i[half:]).astype(F32), F32(end))
     return np.concatenate([lo, hi]).astype(F32)
 
 

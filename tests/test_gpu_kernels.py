@@ -31,8 +31,22 @@ def ok(status, lib):
     assert status == 0, lib.siren_status_string(status)
 
 
+_KEEP = []
+
+
 def to_dev(a, dev, dtype=torch.float32):
-    return torch.from_numpy(np.ascontiguousarray(a, dtype=F32)).to(dev).to(dtype)
+    """Host array -> device tensor.  Kept alive (module list) so a pointer taken from a
+    temporary inside one call can never be recycled by the caching allocator."""
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=F32)).to(dev).to(dtype)
+    _KEEP.append(t)
+    return t
+
+
+@pytest.fixture(autouse=True)
+def _release():
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
 
 
 def bf16_np(t: torch.Tensor) -> np.ndarray:
