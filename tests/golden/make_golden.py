@@ -1,0 +1,199 @@
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE implementation.
+
+Runs only in the build container, where /root/reference (senyuanfan/inr-for-audio) is
+mounted read-only.  Imports the reference's own models.py / utils.py; their top-level
+imports of packages absent here (torchaudio, rff, librosa, torchsummary, matplotlib) are
+satisfied with empty stub modules -- none of them is used by the code paths exercised
+(SURVEY.md §8c).  The reference code itself is never copied: only the numbers it produces
+are written, as small .npz / .json data files.
+
+    python tests/golden/make_golden.py [--trajectory-steps 300]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def import_reference():
+    for name in ["torchaudio", "rff", "librosa", "torchsummary", "matplotlib", "matplotlib.pyplot"]:
+        if name not in sys.modules:
+            try:
+                __import__(name)
+            except ImportError:
+                mod = types.ModuleType(name)
+                if name == "torchsummary":
+                    mod.summary = lambda *a, **k: None
+                if name == "matplotlib":
+                    mod.pyplot = types.ModuleType("matplotlib.pyplot")
+                    sys.modules["matplotlib.pyplot"] = mod.pyplot
+                sys.modules[name] = mod
+    sys.path.insert(0, REF)
+    import models as ref_models  # noqa: E402
+    import utils as ref_utils  # noqa: E402
+    return ref_models, ref_utils
+
+
+def siren(ref_models, H, L, w0, w=30.0, in_dim=1, seed=0):
+    torch.manual_seed(seed)
+    return ref_models.SirenWithSnakeTanh(in_features=in_dim, out_features=1, hidden_features=H,
+                                         num_sine=L, num_snake=0, num_tanh=0, first_omega_0=w0,
+                                         hidden_omega_0=w)
+
+
+def sd_np(model):
+    return {k: v.detach().numpy().astype(np.float32).copy() for k, v in model.state_dict().items()}
+
+
+def summary(sd):
+    return {k: {"shape": list(v.shape), "sum": float(v.astype(np.float64).sum()),
+                "sumsq": float((v.astype(np.float64) ** 2).sum()),
+                "head": v.reshape(-1)[:8].tolist()} for k, v in sd.items()}
+
+
+def fwd_bwd(model, coords, target):
+    model.zero_grad()
+    out = model(coords.reshape(1, -1, coords.shape[-1]))
+    loss = torch.nn.MSELoss()(out, target.reshape(1, -1, 1))
+    loss.backward()
+    grads = {k: p.grad.detach().numpy().copy() for k, p in model.named_parameters()}
+    return out.detach().numpy().reshape(-1), float(loss), grads
+
+
+def restated_loop(model, coords, target, steps, lr=1e-3, min_lr=1e-6):
+    """run.py:156-187 on CPU around the reference model (alpha=0: the STFT term is exactly
+    zero; best_model aliases model, run.py:173)."""
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.8, patience=200,
+                                                       min_lr=min_lr)
+    mse = torch.nn.MSELoss()
+    x = coords.reshape(1, -1, 1)
+    y = target.reshape(1, -1, 1)
+    losses, lrs = [], []
+    for _ in range(steps):
+        out = model(x)
+        loss = mse(out, y)
+        losses.append(float(loss.item()))
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        sched.step(loss)
+        lrs.append(float(sched.get_last_lr()[0]))
+    with torch.no_grad():
+        final = model(x).numpy().reshape(-1)
+    return np.array(losses), np.array(lrs), final
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trajectory-steps", type=int, default=300)
+    args = ap.parse_args()
+    torch.set_num_threads(os.cpu_count() or 1)
+    ref_models, ref_utils = import_reference()
+    from scipy.signal import decimate
+
+    meta = {"generator": "tests/golden/make_golden.py", "torch": torch.__version__,
+            "numpy": np.__version__}
+
+    # --- coordinate grid: utils.py:99-109
+    lin = {f"n{n}": ref_utils.get_coord(n, 1).numpy().reshape(-1) for n in (7, 100, 4097)}
+    np.savez_compressed(os.path.join(OUT, "get_coord.npz"), **lin)
+
+    # --- waveform target: utils.py:111-149 on gt_bach.wav, 1 s
+    wav = os.path.join(REF, "gt_bach.wav")
+    ds = ref_utils.WaveformFitting(wav, duration=1, decimation=1)
+    coords, target = ds[0]
+    from scipy.io import wavfile
+    fs, raw = wavfile.read(wav)
+    raw = raw.astype(np.float32)
+    np.savez_compressed(os.path.join(OUT, "gt_bach_1s.npz"), raw=raw[:2 * fs], fs=np.int64(fs),
+                        target=target.numpy().reshape(-1), coords=coords.numpy().reshape(-1))
+    ds2 = ref_utils.WaveformFitting(wav, duration=2, decimation=2)
+    _, target_d2 = ds2[0]
+    np.savez_compressed(os.path.join(OUT, "gt_bach_2s_dec2.npz"), target=target_d2.numpy().reshape(-1),
+                        sample_rate=np.int64(ds2.sample_rate))
+
+    # --- init: models.py:94-112, 306-386 under torch.manual_seed(0)
+    m3 = siren(ref_models, 256, 2, 1000.0)
+    np.savez_compressed(os.path.join(OUT, "init_3x256_seed0.npz"), **sd_np(m3))
+    m5 = siren(ref_models, 1024, 4, 3000.0)
+    json.dump(summary(sd_np(m5)), open(os.path.join(OUT, "init_5x1024_seed0_summary.json"), "w"), indent=1)
+    m_st = siren(ref_models, 512, 4, 3000.0, in_dim=2, seed=3)
+    json.dump(summary(sd_np(m_st)), open(os.path.join(OUT, "init_5x512_in2_seed3_summary.json"), "w"),
+              indent=1)
+
+    # --- one forward/backward (models.py:388-394, run.py:168,185) on a 2100-point subset
+    idx = np.arange(0, 44100, 21)
+    c_sub, t_sub = coords[idx], target[idx]
+    fb = {}
+    for w0 in (1000.0, 22000.0):
+        m = siren(ref_models, 256, 2, w0)
+        out, loss, grads = fwd_bwd(m, c_sub, t_sub)
+        acts = m.forward_with_activations(c_sub.reshape(1, -1, 1))
+        # SineLayer entries alternate (omega*linear, sin(.)) -- models.py:404-421
+        sine = [v.detach().numpy().reshape(-1, v.shape[-1])[:16] for k, v in acts.items()
+                if "SineLayer" in k]
+        tag = f"w{int(w0)}"
+        fb[f"{tag}_out"] = out
+        fb[f"{tag}_loss"] = np.array([loss])
+        for k, g in grads.items():
+            fb[f"{tag}_grad_{k}"] = g
+        for j in range(len(sine) // 2):
+            fb[f"{tag}_preact{j}"] = sine[2 * j]
+            fb[f"{tag}_sin{j}"] = sine[2 * j + 1]
+        if w0 == 1000.0:
+            opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+            opt.step()
+            for k, p in m.named_parameters():
+                fb[f"{tag}_adam1_{k}"] = p.detach().numpy().copy()
+    fb["subset_idx"] = idx
+    np.savez_compressed(os.path.join(OUT, "fwd_bwd_3x256.npz"), **fb)
+
+    # --- ReduceLROnPlateau trace (run.py:117,187)
+    rng = np.random.default_rng(0)
+    seq = np.concatenate([np.linspace(1.0, 0.5, 300), 0.5 + 0.01 * rng.random(1200)])
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.Adam([p], lr=1e-3)
+    sch = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.8, patience=200, min_lr=2e-4)
+    lrs = []
+    for v in seq:
+        sch.step(float(np.float32(v)))
+        lrs.append(sch.get_last_lr()[0])
+    json.dump({"loss": [float(np.float32(v)) for v in seq], "lr": lrs, "patience": 200, "factor": 0.8,
+               "min_lr": 2e-4, "lr0": 1e-3}, open(os.path.join(OUT, "plateau_trace.json"), "w"))
+
+    # --- SNR metrics: utils.py:77-97, run.py:302-335 quirks
+    tgt = target.numpy().reshape(-1)
+    snr = {
+        "perfect_fit_reported_1s": float(ref_utils.calculate_snr(decimate(raw[:fs], q=1) + 1e-10, tgt)),
+        "lowpass_only_1s": float(ref_utils.calculate_snr(decimate(raw[:fs], q=1) + 1e-10, raw[:fs])),
+        "target_vs_half": float(ref_utils.calculate_snr(tgt, 0.5 * tgt)),
+        "target_vs_noisy": float(ref_utils.calculate_snr(tgt, tgt + 0.01 * np.sin(np.arange(fs)))),
+    }
+    json.dump(snr, open(os.path.join(OUT, "snr_cases.json"), "w"), indent=1)
+
+    # --- full-batch trajectory: run.py:156-190, SIREN 3x256, omega0 = 1000, gt_bach 1 s
+    if args.trajectory_steps > 0:
+        m = siren(ref_models, 256, 2, 1000.0)
+        losses, lrs, final = restated_loop(m, coords, target, args.trajectory_steps)
+        json.dump({"steps": args.trajectory_steps, "omega0": 1000.0, "hidden": 256, "num_sine": 2,
+                   "seed": 0, "loss": losses.tolist(), "lr": lrs.tolist(),
+                   "snr_target": float(ref_utils.calculate_snr(tgt, final)),
+                   "snr_reported": float(ref_utils.calculate_snr(decimate(raw[:fs], q=1) + 1e-10, final))},
+                  open(os.path.join(OUT, "trajectory_3x256_w1000.json"), "w"))
+        np.savez_compressed(os.path.join(OUT, "trajectory_3x256_w1000_final.npz"), out=final.astype(np.float32))
+    json.dump(meta, open(os.path.join(OUT, "meta.json"), "w"), indent=1)
+    print("golden fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()

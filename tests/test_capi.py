@@ -1,0 +1,65 @@
+"""The C-ABI library loads on a GPU-less host and exports exactly what include/siren_hip.h
+declares; argument validation returns status codes without touching the device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "siren_hip.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?(?:int|int32_t|int64_t|char\s*\*)\s*\**\s*(siren_\w+)\s*\(",
+                          src, flags=re.M))
+
+
+def test_header_parses():
+    names = declared()
+    assert {"siren_train_step", "siren_apply_update", "siren_inner_fwd", "siren_inner_bwd_dw",
+            "siren_adam_step", "siren_plateau_step"} <= names
+    assert len(names) >= 24
+
+
+def test_library_exports_every_declared_symbol(lib):
+    for name in declared():
+        assert hasattr(lib, name), name
+
+
+def test_binding_table_matches_header(lib):
+    from inr_for_audio_amd import _lib
+    assert set(_lib._SIGS) == declared()
+
+
+def test_host_only_helpers(lib):
+    assert lib.siren_abi_version() == 1
+    assert lib.siren_status_string(0) == b"ok"
+    assert b"shape" in lib.siren_status_string(1001)
+    assert lib.siren_default_splits(1 << 20, 1024) == 16
+    assert lib.siren_default_splits(44160, 256) >= 1
+    assert lib.siren_slab_floats(1024, 16) == 16 * 1024 * 1024
+
+
+def test_validation_without_device(lib):
+    from inr_for_audio_amd._lib import SirenBatch, SirenGrads, SirenNet
+    net = SirenNet()
+    assert lib.siren_train_step(None, None, None, None) == 1002          # NULL net
+    net.in_dim, net.hidden, net.n_inner = 3, 256, 2
+    assert lib.siren_train_step(ctypes.byref(net), ctypes.byref(SirenGrads()),
+                                ctypes.byref(SirenBatch()), None) == 1003  # in_dim 3 unsupported
+    net.in_dim, net.hidden = 1, 384
+    assert lib.siren_forward(ctypes.byref(net), ctypes.byref(SirenBatch()), None) == 1001
+    assert lib.siren_inner_fwd(None, None, None, ctypes.c_float(30), 128, 256, None, None, None, None,
+                               None) == 1002
+    assert lib.siren_inner_bwd_dw(1, 1, 100, 256, 1, 1, None) == 1001    # rows % 64
+    assert lib.siren_first_fwd(1, 3, 1, 1, ctypes.c_float(1.0), 128, 256, 1, None) == 1003
+
+
+@pytest.mark.parametrize("hidden", [128, 256, 512, 1024])
+def test_supported_hidden_sizes_validate(lib, hidden):
+    # only shape checks run (NULL outputs make it return before any launch)
+    assert lib.siren_head_bwd(None, None, None, None, ctypes.c_float(30), 128, hidden, None, None, None,
+                              None) == 1002

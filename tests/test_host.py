@@ -1,0 +1,140 @@
+"""Host-side logic of the package (no GPU): reference-compatible construction and init,
+parameter layout, configuration validation, data prep and metrics, train() API."""
+import inspect
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _model(H=256, L=2, w0=1000.0, in_dim=1, seed=0):
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(seed)
+    return SirenWithSnakeTanh(in_features=in_dim, out_features=1, hidden_features=H, num_sine=L,
+                              num_snake=0, num_tanh=0, first_omega_0=w0, hidden_omega_0=30)
+
+
+def test_init_bit_exact_with_reference_3x256():
+    ref = np.load(os.path.join(G, "init_3x256_seed0.npz"))
+    sd = _model().state_dict()
+    assert list(sd.keys()) == list(ref.files)
+    for k in ref.files:
+        assert np.array_equal(sd[k].numpy(), ref[k]), k
+
+
+@pytest.mark.parametrize("fname,H,L,in_dim,seed", [("init_5x1024_seed0_summary.json", 1024, 4, 1, 0),
+                                                   ("init_5x512_in2_seed3_summary.json", 512, 4, 2, 3)])
+def test_init_matches_reference_large(fname, H, L, in_dim, seed):
+    ref = json.load(open(os.path.join(G, fname)))
+    sd = _model(H, L, 3000.0, in_dim, seed).state_dict()
+    assert list(sd.keys()) == list(ref.keys())
+    for k, r in ref.items():
+        v = sd[k].numpy().astype(np.float64)
+        assert list(v.shape) == r["shape"]
+        assert v.reshape(-1)[:8].astype(np.float32).tolist() == r["head"]
+        assert v.sum() == pytest.approx(r["sum"], rel=1e-12, abs=1e-12)
+        assert (v ** 2).sum() == pytest.approx(r["sumsq"], rel=1e-12)
+
+
+def test_param_layout():
+    from inr_for_audio_amd.engine import SEG_ALIGN, ParamLayout
+    m = _model(1024, 4)
+    lay = ParamLayout(m)
+    assert lay.names == list(m.state_dict().keys())
+    assert all(o % SEG_ALIGN == 0 for o in lay.offsets)
+    assert sum(lay.numels) == 4201473          # 5x1024 parameter count
+    assert lay.sse_offset == lay.n_params and lay.flat_len == lay.n_params + SEG_ALIGN
+    flat = torch.arange(lay.flat_len, dtype=torch.float32)
+    for i, shp in enumerate(lay.shapes):
+        v = lay.view(flat, i)
+        assert tuple(v.shape) == shp and int(v.reshape(-1)[0]) == lay.offsets[i]
+
+
+def test_hip_spec_validation():
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    spec = _model(256, 2, 22000.0).hip_spec()
+    assert (spec.in_dim, spec.hidden, spec.n_inner, spec.omega0, spec.omega) == (1, 256, 2, 22000.0, 30.0)
+    bad = [dict(num_snake=2), dict(num_tanh=1), dict(first_linear=True), dict(last_linear=False),
+           dict(hidden_features=384), dict(num_sine=0), dict(in_features=3)]
+    for kw in bad:
+        args = dict(in_features=1, out_features=1, hidden_features=256, num_sine=2, num_snake=0, num_tanh=0)
+        args.update(kw)
+        with pytest.raises(NotImplementedError):
+            SirenWithSnakeTanh(**args).hip_spec()
+
+
+def test_reference_default_snake_config_constructs():
+    """train()'s defaults (num_sine=2, num_snake=2, a_initial=0.5) build the reference's
+    module tree and parameter names even though the HIP path rejects Snake."""
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    m = SirenWithSnakeTanh(1, 1, 256, 2, 2, 0, a_initial=0.5)
+    names = list(m.state_dict().keys())
+    assert names[-2:] == ["net.7.weight", "net.7.bias"] and "net.4.a" in names
+
+
+def test_shard_range_partitions():
+    from inr_for_audio_amd.engine import shard_range
+    for n in (1, 7, 1000, 28_800_000):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def test_train_signature_matches_reference():
+    """run.py:30 -- same positional/keyword parameters and defaults, extras keyword-only."""
+    from inr_for_audio_amd.run import train
+    ref = [("experiment_path", None), ("tag", None), ("inst", None), ("duration", None),
+           ("num_channels", 1), ("method", "wave"), ("arch", "mlp"), ("loss_mode", "mse"), ("mode", None),
+           ("decimation", 1), ("bwe", False), ("num_hidden_features", 256), ("num_sine", 2),
+           ("num_snake", 2), ("num_tanh", 0), ("num_freq", None), ("omega", 22000),
+           ("first_linear", False), ("last_linear", True), ("hidden_omega", 30), ("a_initial", 0.5),
+           ("total_steps", 20000), ("learning_rate", 1e-3), ("min_learning_rate", 1e-6), ("alpha", 0.0),
+           ("prev_ckpt_path", None), ("visualization", False)]
+    params = inspect.signature(train).parameters
+    pos = [p for p in params.values() if p.kind == p.POSITIONAL_OR_KEYWORD]
+    assert [p.name for p in pos] == [r[0] for r in ref]
+    for p, (name, default) in zip(pos, ref):
+        if default is not None:
+            assert p.default == default, name
+    assert all(p.kind == p.KEYWORD_ONLY for p in params.values() if p not in pos)
+
+
+def test_waveform_fitting_and_reported_snr(tmp_path):
+    from scipy.io import wavfile
+    from inr_for_audio_amd import utils
+    g = np.load(os.path.join(G, "gt_bach_1s.npz"))
+    fs = int(g["fs"])
+    wav = str(tmp_path / "x.wav")
+    wavfile.write(wav, fs, g["raw"])
+    ds = utils.WaveformFitting(wav, duration=1)
+    coords, amp = ds[0]
+    assert np.array_equal(amp.numpy().reshape(-1), g["target"])
+    assert np.array_equal(coords.numpy().reshape(-1), g["coords"])
+    ref, fs2 = utils.load_mono_like_librosa(wav)
+    snr = json.load(open(os.path.join(G, "snr_cases.json")))
+    assert abs(utils.reported_snr(ref, fs2, g["target"], 1) - snr["perfect_fit_reported_1s"]) < 1e-5
+    d2 = utils.WaveformFitting(wav, duration=2, decimation=2)
+    ref2 = np.load(os.path.join(G, "gt_bach_2s_dec2.npz"))
+    assert np.allclose(d2.amplitude().numpy().reshape(-1), ref2["target"], atol=1e-7)
+    assert d2.sample_rate == int(ref2["sample_rate"])
+
+
+def test_unsupported_train_options_raise(tmp_path):
+    from inr_for_audio_amd.run import train
+    for kw in (dict(method="mdct"), dict(arch="kan"), dict(loss_mode="mae"), dict(alpha=0.5)):
+        with pytest.raises(NotImplementedError):
+            train(str(tmp_path), "t", "x", 1, **kw)
+
+
+def test_package_never_imports_oracle():
+    root = os.path.join(os.path.dirname(G), "..", "inr-for-audio_amd")
+    for dirpath, _, files in os.walk(root):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in src.replace("# oracle", ""), f
