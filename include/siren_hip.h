@@ -81,7 +81,7 @@ typedef struct siren_batch {
   const float* coords;   /* [rows][in]  */
   const float* target;   /* [rows]      */
   uint16_t* Y[SIREN_MAX_INNER + 1];  /* Y[0..L] bf16 [rows][H]: layer outputs sin(.)  */
-  uint16_t* C[SIREN_MAX_INNER + 1];  /* C[1..L] bf16 [rows][H]: cos(.) of inner layers */
+  uint16_t* C[SIREN_MAX_INNER + 1];  /* C[0..L] bf16 [rows][H]: cos(.) of every layer  */
   uint16_t* dZ[2];       /* bf16 [rows][H] ping-pong pre-activation gradients   */
   float* out;            /* [rows] model output                                 */
   float* g;              /* [rows] dLoss/dout                                   */
@@ -94,7 +94,11 @@ typedef struct siren_batch {
   float* slab;           /* [splits][H][H]                                      */
 } siren_batch;
 
-/* Workspace sizing helpers (element counts). */
+/* Workspace sizing / tiling helpers.  siren_nt_tile: tile edge the NT GEMMs use for
+ * `rows` coordinates (partial-sum buffers then hold rows/tile rows and head partials
+ * hidden/tile rows); siren_dw_tile: tile edge of the weight-gradient GEMM. */
+int32_t siren_nt_tile(int32_t rows, int32_t hidden);
+int32_t siren_dw_tile(int32_t rows, int32_t hidden);
 int32_t siren_default_splits(int32_t rows, int32_t hidden);
 int64_t siren_slab_floats(int32_t hidden, int32_t splits);
 
@@ -122,9 +126,10 @@ int siren_apply_update(const siren_net* net, float* params, const float* grads_f
 /* ---- individual kernels (parity tests call these one by one) ------------------------ */
 /* utils.py:99-109 get_coord: torch.linspace(-1,1,n_total) at [offset, offset+rows) */
 int siren_coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, void* stream);
-/* models.py:114-115 first SineLayer: Y0 = sin(omega0*(t W0^T + b0)) -> bf16 */
+/* models.py:114-115 first SineLayer: a0 = omega0*(t W0^T + b0) in fp32, Y0 = sin a0 and
+ * C0 = cos a0 (one fp32 sincosf range reduction) -> bf16 */
 int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float* b0, float omega0,
-                    int32_t rows, int32_t hidden, uint16_t* Y0, void* stream);
+                    int32_t rows, int32_t hidden, uint16_t* Y0, uint16_t* C0, void* stream);
 /* models.py:114-115 hidden SineLayer: Y = sin(omega(X W^T + b)), C = cos(.); optional head
  * partial dot (models.py:374-381) when head_w != NULL */
 int siren_inner_fwd(const uint16_t* X, const uint16_t* Wb, const float* b, float omega, int32_t rows,
@@ -141,15 +146,17 @@ int siren_head_bwd(const uint16_t* C, const uint16_t* Y, const float* g, const f
 /* autograd addmm dX + sin/omega backward of the layer below: dZprev = omega*cos*(dZ W) */
 int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTb, const uint16_t* Cprev, float omega_prev,
                        int32_t rows, int32_t hidden, uint16_t* dZprev, float* db_part, void* stream);
-/* same into the fp32 first layer: partials [rows/128][1+in][H] of dZ0 and dZ0*t_j */
-int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTb1, const float* t, int32_t in_dim,
-                       const float* W0, const float* b0, float omega0, int32_t rows, int32_t hidden,
-                       float* part, void* stream);
-/* autograd addmm dW: slab[s] = partial dZ^T Y over coordinate slice s */
+/* same into the fp32 first layer (C0 from siren_first_fwd): partials [rows/128][1+in][H]
+ * of dZ0 and dZ0*t_j; dZ0 itself is never stored */
+int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTb1, const uint16_t* C0, const float* t,
+                       int32_t in_dim, float omega0, int32_t rows, int32_t hidden, float* part,
+                       void* stream);
+/* autograd addmm dW: slab[s] = partial dZ^T Y over coordinate slice s, tile edge 128/256
+ * (0 = siren_dw_tile(rows, hidden)); siren_dw_reduce must get the same tile. */
 int siren_inner_bwd_dw(const uint16_t* Y, const uint16_t* dZ, int32_t rows, int32_t hidden,
-                       int32_t splits, float* slab, void* stream);
-int siren_dw_reduce(const float* slab, int32_t splits, int32_t hidden, float* grad, int32_t accumulate,
-                    void* stream);
+                       int32_t splits, int32_t tile, float* slab, void* stream);
+int siren_dw_reduce(const float* slab, int32_t splits, int32_t hidden, int32_t tile, float* grad,
+                    int32_t accumulate, void* stream);
 int siren_col_reduce(const float* part, int64_t row_stride, int32_t nrows, int32_t ncols, float* out,
                      int32_t out_stride, int32_t accumulate, float* tmp, void* stream);
 /* torch.optim.Adam step over a flat fp32 vector (run.py:186) */
@@ -172,6 +179,10 @@ enum siren_prof_kind {
   SIREN_PROF_BWD_DX = 4, SIREN_PROF_BWD_DX0 = 5, SIREN_PROF_REDUCE = 6, SIREN_PROF_UPDATE = 7,
   SIREN_PROF_NKINDS = 8
 };
+/* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
+ * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge. */
+enum siren_option { SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1 };
+int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);
 int siren_profile_reset(void);
 int siren_profile_read(int32_t kind, double* total_ms, int64_t* count);

@@ -81,20 +81,22 @@ _SIGS = {
                                           ctypes.POINTER(_p), ctypes.POINTER(_p), ctypes.POINTER(_p),
                                           _p, _p, ctypes.c_double, _p, _p, _i64, _p]),
     "siren_coords_fill": (ctypes.c_int, [_p, _i64, _i64, _i64, _p]),
-    "siren_first_fwd": (ctypes.c_int, [_p, _i32, _p, _p, ctypes.c_float, _i32, _i32, _p, _p]),
+    "siren_first_fwd": (ctypes.c_int, [_p, _i32, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p]),
     "siren_inner_fwd": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p]),
     "siren_head_loss": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _i32, ctypes.c_double, _p, _p, _p, _p,
                                        _p]),
     "siren_head_bwd": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p]),
     "siren_inner_bwd_dx": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p]),
-    "siren_first_bwd_dx": (ctypes.c_int, [_p, _p, _p, _i32, _p, _p, ctypes.c_float, _i32, _i32, _p,
-                                          _p]),
-    "siren_inner_bwd_dw": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _p, _p]),
-    "siren_dw_reduce": (ctypes.c_int, [_p, _i32, _i32, _p, _i32, _p]),
+    "siren_first_bwd_dx": (ctypes.c_int, [_p, _p, _p, _p, _i32, ctypes.c_float, _i32, _i32, _p, _p]),
+    "siren_inner_bwd_dw": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _p, _p]),
+    "siren_dw_reduce": (ctypes.c_int, [_p, _i32, _i32, _i32, _p, _i32, _p]),
+    "siren_nt_tile": (_i32, [_i32, _i32]),
+    "siren_dw_tile": (_i32, [_i32, _i32]),
     "siren_col_reduce": (ctypes.c_int, [_p, _i64, _i32, _i32, _p, _i32, _i32, _p, _p]),
     "siren_adam_step": (ctypes.c_int, [_p, _p, _p, _p, _i64, _p, _p]),
     "siren_plateau_step": (ctypes.c_int, [_p, _p, ctypes.c_double, _p, _p, _i64, _p]),
     "siren_cast_weight": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p]),
+    "siren_set_option": (ctypes.c_int, [_i32, _i32]),
     "siren_profile_enable": (ctypes.c_int, [_i32]),
     "siren_profile_reset": (ctypes.c_int, []),
     "siren_profile_read": (ctypes.c_int, [_i32, ctypes.POINTER(ctypes.c_double),

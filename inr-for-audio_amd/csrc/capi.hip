@@ -69,7 +69,7 @@ int check_batch(const siren_net* n, const siren_batch* b, bool train) {
   if (!b->coords || !b->out || !b->head_part || !b->g || !b->sse_part || !b->gsum_part)
     return SIREN_ERR_NULL;
   for (int i = 0; i <= n->n_inner; ++i)
-    if (!b->Y[i] || (i > 0 && !b->C[i])) return SIREN_ERR_NULL;
+    if (!b->Y[i] || !b->C[i]) return SIREN_ERR_NULL;
   if (train) {
     if (!b->target || !b->dZ[0] || !b->dZ[1] || !b->col_part || !b->col_part2 || !b->red_tmp ||
         !b->slab)
@@ -82,12 +82,14 @@ int check_batch(const siren_net* n, const siren_batch* b, bool train) {
 // forward through all layers + head partials; returns hip status
 hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s) {
   const int R = b->rows, H = n->hidden, L = n->n_inner;
-  SIREN_PROF(SIREN_PROF_FIRST_FWD, s, first_fwd(b->coords, n->in_dim, n->W0, n->b0, n->omega0, R, H, B(b->Y[0]), s));
+  SIREN_PROF(SIREN_PROF_FIRST_FWD, s, first_fwd(b->coords, n->in_dim, n->W0, n->b0, n->omega0, R, H, B(b->Y[0]),
+                                                B(b->C[0]), s));
   for (int i = 0; i < L; ++i) {
     NtParams p = {};
     p.X = B(b->Y[i]);
     p.W = B(n->Wb[i]);
     p.M = R; p.N = H; p.K = H;
+    p.tile = nt_choose_tile(R, H);
     p.omega = n->omega;
     p.bias = n->b[i];
     p.Y = B(b->Y[i + 1]);
@@ -116,10 +118,15 @@ const char* siren_status_string(int status) {
   return hipGetErrorString((hipError_t)status);
 }
 
+int32_t siren_nt_tile(int32_t rows, int32_t hidden) { return nt_choose_tile(rows, hidden); }
+int32_t siren_dw_tile(int32_t rows, int32_t hidden) { return tn_choose_tile(rows, hidden, hidden); }
+
 int32_t siren_default_splits(int32_t rows, int32_t hidden) {
-  // aim for ~1024 blocks (4 per CU at 2 resident per CU) without slices thinner than 8 K-steps
-  const int ntile = (hidden / 128) * (hidden / 128);
-  int splits = 1024 / (ntile > 0 ? ntile : 1);
+  // aim for ~1024 blocks-worth of tiles (4 waves of resident blocks) without slices thinner
+  // than 8 K-steps
+  const int tile = tn_choose_tile(rows, hidden, hidden);
+  const int ntile = (hidden / tile) * (hidden / tile);
+  int splits = (tile == 256 ? 512 : 1024) / (ntile > 0 ? ntile : 1);
   const int nks = rows / 64;
   const int max_splits = nks / 8 > 0 ? nks / 8 : 1;
   if (splits > max_splits) splits = max_splits;
@@ -138,7 +145,8 @@ int siren_forward(const siren_net* net, siren_batch* batch, void* stream) {
   hipStream_t s = S(stream);
   SIREN_TRY(run_forward(net, batch, s));
   // out = sum of head partials + bias (g/sse unused at inference: n_valid = 0 path)
-  SIREN_TRY(head_loss(batch->head_part, net->hidden / 128, batch->rows, net->b_head, batch->out,
+  SIREN_TRY(head_loss(batch->head_part, net->hidden / nt_choose_tile(batch->rows, net->hidden),
+                      batch->rows, net->b_head, batch->out,
                       0, 0.f, batch->out, batch->g, batch->sse_part, batch->gsum_part, s));
   return SIREN_OK;
 }
@@ -153,6 +161,8 @@ static int check_grads(const siren_net* net, const siren_grads* gr) {
 // autograd of models.py:388-394 given dLoss/dout in batch->g (rows >= n_valid are zero)
 static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch* b, hipStream_t s) {
   const int R = b->rows, H = net->hidden, L = net->n_inner, in = net->in_dim;
+  const int ntile = nt_choose_tile(R, H), tntile = tn_choose_tile(R, H, H);
+  const int prow = R / ntile;  // partial rows written by the NT_DX / NT_DX0 epilogues
   SIREN_PROF(SIREN_PROF_HEAD, s, head_bwd(B(b->C[L]), B(b->Y[L]), b->g, net->w_head, net->omega, R, H,
                                           B(b->dZ[0]), b->col_part, b->col_part2, s));
   SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part2, H, R / 128, H, gr->w_head, 1, 1, b->red_tmp, s));
@@ -165,33 +175,34 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
     tp.dZ = B(b->dZ[cur]);
     tp.R = R; tp.Hin = H; tp.Hout = H;
     tp.splits = b->splits;
+    tp.tile = tntile;
     tp.slab = b->slab;
     SIREN_PROF(SIREN_PROF_BWD_DW, s, gemm_tn_dw(tp, s));
-    SIREN_PROF(SIREN_PROF_REDUCE, s, dw_reduce(b->slab, b->splits, H, H, gr->W[i], 1, s));
+    SIREN_PROF(SIREN_PROF_REDUCE, s, dw_reduce(b->slab, b->splits, H, H, tntile, gr->W[i], 1, s));
 
     NtParams p = {};
     p.X = B(b->dZ[cur]);
     p.W = B(net->WTb[i]);
     p.M = R; p.N = H; p.K = H;
+    p.tile = ntile;
     p.colsum_part = b->col_part;
     if (i > 0) {
       p.omega = net->omega;
       p.Cprev = B(b->C[i]);
       p.dZ = B(b->dZ[cur ^ 1]);
       SIREN_PROF(SIREN_PROF_BWD_DX, s, gemm_nt(NT_DX, false, p, s));
-      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, R / 128, H, gr->b[i - 1], 1, 1, b->red_tmp, s));
+      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, prow, H, gr->b[i - 1], 1, 1, b->red_tmp, s));
       cur ^= 1;
     } else {
       p.omega = net->omega0;
+      p.Cprev = B(b->C[0]);
       p.t = b->coords;
-      p.W0 = net->W0;
-      p.b0 = net->b0;
       p.in_dim = in;
       SIREN_PROF(SIREN_PROF_BWD_DX0, s, gemm_nt(NT_DX0, false, p, s));
       const int64_t rs = (int64_t)(1 + in) * H;
-      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, rs, R / 128, H, gr->b0, 1, 1, b->red_tmp, s));
+      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, rs, prow, H, gr->b0, 1, 1, b->red_tmp, s));
       for (int j = 0; j < in; ++j)
-        SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + (int64_t)(1 + j) * H, rs, R / 128, H,
+        SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + (int64_t)(1 + j) * H, rs, prow, H,
                                                     gr->W0 + j, in, 1, b->red_tmp, s));
     }
   }
@@ -212,7 +223,8 @@ int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b
   // ---- forward (models.py:388-394) + MSE (run.py:168) ----
   SIREN_TRY(run_forward(net, b, s));
   const float gscale = (float)(2.0 / b->n_total);  // MSELoss mean backward: 2/N
-  SIREN_PROF(SIREN_PROF_HEAD, s, head_loss(b->head_part, H / 128, R, net->b_head, b->target, b->n_valid,
+  SIREN_PROF(SIREN_PROF_HEAD, s, head_loss(b->head_part, H / nt_choose_tile(R, H), R, net->b_head,
+                                           b->target, b->n_valid,
                                            gscale, b->out, b->g, b->sse_part, b->gsum_part, s));
   const int nsum = (R + 255) / 256;
   SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->sse_part, nsum, gr->sse, 1, s));
@@ -259,11 +271,11 @@ int siren_coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, v
 }
 
 int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float* b0, float omega0,
-                    int32_t rows, int32_t hidden, uint16_t* Y0, void* stream) {
-  if (!t || !W0 || !b0 || !Y0) return SIREN_ERR_NULL;
+                    int32_t rows, int32_t hidden, uint16_t* Y0, uint16_t* C0, void* stream) {
+  if (!t || !W0 || !b0 || !Y0 || !C0) return SIREN_ERR_NULL;
   if (in_dim < 1 || in_dim > 2) return SIREN_ERR_CONFIG;
   if (rows < 0 || hidden % 4) return SIREN_ERR_SHAPE;
-  return (int)first_fwd(t, in_dim, W0, b0, omega0, rows, hidden, B(Y0), S(stream));
+  return (int)first_fwd(t, in_dim, W0, b0, omega0, rows, hidden, B(Y0), B(C0), S(stream));
 }
 
 int siren_inner_fwd(const uint16_t* X, const uint16_t* Wb, const float* b, float omega, int32_t rows,
@@ -274,6 +286,7 @@ int siren_inner_fwd(const uint16_t* X, const uint16_t* Wb, const float* b, float
   if (head_w && !head_part) return SIREN_ERR_NULL;
   NtParams p = {};
   p.X = B(X); p.W = B(Wb); p.M = rows; p.N = hidden; p.K = hidden;
+  p.tile = nt_choose_tile(rows, hidden);
   p.omega = omega; p.bias = b; p.Y = B(Y); p.C = B(C);
   p.head_w = head_w; p.head_part = head_part;
   return (int)gemm_nt(NT_FWD, head_w != nullptr, p, S(stream));
@@ -304,37 +317,42 @@ int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTb, const uint16_t* 
   if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
   NtParams p = {};
   p.X = B(dZ); p.W = B(WTb); p.M = rows; p.N = hidden; p.K = hidden;
+  p.tile = nt_choose_tile(rows, hidden);
   p.omega = omega_prev; p.Cprev = B(Cprev); p.dZ = B(dZprev); p.colsum_part = db_part;
   return (int)gemm_nt(NT_DX, false, p, S(stream));
 }
 
-int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTb1, const float* t, int32_t in_dim,
-                       const float* W0, const float* b0, float omega0, int32_t rows, int32_t hidden,
-                       float* part, void* stream) {
-  if (!dZ1 || !WTb1 || !t || !W0 || !b0 || !part) return SIREN_ERR_NULL;
+int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTb1, const uint16_t* C0, const float* t,
+                       int32_t in_dim, float omega0, int32_t rows, int32_t hidden, float* part,
+                       void* stream) {
+  if (!dZ1 || !WTb1 || !C0 || !t || !part) return SIREN_ERR_NULL;
   if (in_dim < 1 || in_dim > 2) return SIREN_ERR_CONFIG;
   if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
   NtParams p = {};
   p.X = B(dZ1); p.W = B(WTb1); p.M = rows; p.N = hidden; p.K = hidden;
-  p.omega = omega0; p.t = t; p.W0 = W0; p.b0 = b0; p.in_dim = in_dim; p.colsum_part = part;
+  p.tile = nt_choose_tile(rows, hidden);
+  p.omega = omega0; p.Cprev = B(C0); p.t = t; p.in_dim = in_dim; p.colsum_part = part;
   return (int)gemm_nt(NT_DX0, false, p, S(stream));
 }
 
 int siren_inner_bwd_dw(const uint16_t* Y, const uint16_t* dZ, int32_t rows, int32_t hidden,
-                       int32_t splits, float* slab, void* stream) {
+                       int32_t splits, int32_t tile, float* slab, void* stream) {
   if (!Y || !dZ || !slab) return SIREN_ERR_NULL;
   if (!hidden_ok(hidden) || rows <= 0 || rows % 64 || splits < 1) return SIREN_ERR_SHAPE;
+  if (tile != 0 && tile != 128 && tile != 256) return SIREN_ERR_CONFIG;
   TnParams p = {};
   p.Y = B(Y); p.dZ = B(dZ); p.R = rows; p.Hin = hidden; p.Hout = hidden; p.splits = splits;
+  p.tile = tile ? tile : tn_choose_tile(rows, hidden, hidden);
   p.slab = slab;
   return (int)gemm_tn_dw(p, S(stream));
 }
 
-int siren_dw_reduce(const float* slab, int32_t splits, int32_t hidden, float* grad, int32_t accumulate,
-                    void* stream) {
+int siren_dw_reduce(const float* slab, int32_t splits, int32_t hidden, int32_t tile, float* grad,
+                    int32_t accumulate, void* stream) {
   if (!slab || !grad) return SIREN_ERR_NULL;
   if (!hidden_ok(hidden) || splits < 1) return SIREN_ERR_SHAPE;
-  return (int)dw_reduce(slab, splits, hidden, hidden, grad, accumulate, S(stream));
+  if (tile != 128 && tile != 256) return SIREN_ERR_CONFIG;
+  return (int)dw_reduce(slab, splits, hidden, hidden, tile, grad, accumulate, S(stream));
 }
 
 int siren_col_reduce(const float* part, int64_t row_stride, int32_t nrows, int32_t ncols, float* out,
@@ -363,6 +381,15 @@ int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wb,
   if (!W || !Wb || !WTb) return SIREN_ERR_NULL;
   if (h_out % 64 || h_in % 64) return SIREN_ERR_SHAPE;
   return (int)cast_weight(W, h_out, h_in, B(Wb), B(WTb), S(stream));
+}
+
+int siren_set_option(int32_t option, int32_t value) {
+  if (value != 0 && value != 128 && value != 256) return SIREN_ERR_CONFIG;
+  switch (option) {
+    case SIREN_OPT_NT_TILE: gemm_nt_set_tile(value); return SIREN_OK;
+    case SIREN_OPT_TN_TILE: gemm_tn_set_tile(value); return SIREN_OK;
+  }
+  return SIREN_ERR_CONFIG;
 }
 
 // ---- profiling API ---------------------------------------------------------------------

@@ -45,7 +45,7 @@ hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, 
 // K=2: fma(t1, w1, t0*w0) + b) and sinf does a full-precision range reduction.
 __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const float* __restrict__ W0,
                                  const float* __restrict__ b0, float omega0, int R, int H,
-                                 bf16* __restrict__ Y0) {
+                                 bf16* __restrict__ Y0, bf16* __restrict__ C0) {
   const int hq = H >> 2;
   const int64_t total = (int64_t)R * hq;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -54,23 +54,24 @@ __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const 
     const int n = (int)(idx - m * hq) * 4;
     const float t0 = t[m * in_dim];
     const float t1 = (in_dim > 1) ? t[m * in_dim + 1] : 0.f;
-    float y[4];
+    float y[4], c[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float z;
       if (in_dim == 1) z = __builtin_fmaf(t0, W0[n + r], b0[n + r]);
       else z = __builtin_fmaf(t1, W0[(n + r) * 2 + 1], t0 * W0[(n + r) * 2]) + b0[n + r];
-      y[r] = sinf(omega0 * z);
+      sincosf(omega0 * z, &y[r], &c[r]);
     }
     *(bf16x4*)(Y0 + m * H + n) = pack4(y[0], y[1], y[2], y[3]);
+    *(bf16x4*)(C0 + m * H + n) = pack4(c[0], c[1], c[2], c[3]);
   }
 }
 
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
-                     int R, int H, bf16* Y0, hipStream_t s) {
+                     int R, int H, bf16* Y0, bf16* C0, hipStream_t s) {
   if (H % 4 || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
   hipLaunchKernelGGL(first_fwd_kernel, dim3(grid_for((int64_t)R * (H / 4), 256)), dim3(256), 0, s, t,
-                     in_dim, W0, b0, omega0, R, H, Y0);
+                     in_dim, W0, b0, omega0, R, H, Y0, C0);
   return hipGetLastError();
 }
 

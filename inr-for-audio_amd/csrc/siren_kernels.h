@@ -14,6 +14,7 @@ struct NtParams {
   const bf16* X;  // [M][K]
   const bf16* W;  // [N][K]
   int M, N, K;
+  int tile;       // 128 or 256 (nt_choose_tile): partials are per tile-row / tile-column
   float omega;  // FWD: this layer's omega; DX: omega of the layer below; DX0: omega_0
   // NT_FWD
   const float* bias;    // [N]
@@ -25,32 +26,35 @@ struct NtParams {
   const bf16* Cprev;    // [M][N]  cos of the layer below (NT_DX)
   bf16* dZ;             // [M][N]  (NT_DX)
   float* colsum_part;   // NT_DX: [M/128][N];  NT_DX0: [M/128][1+in][N]
-  // NT_DX0
+  // NT_DX0 (Cprev = cos of the first layer)
   const float* t;       // [M][in]
-  const float* W0;      // [N][in]
-  const float* b0;      // [N]
   int in_dim;
 };
 
+int nt_choose_tile(int M, int N);
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s);
+void gemm_nt_set_tile(int tile);  // 0 = auto, 128, 256 (A/B measurement)
+void gemm_tn_set_tile(int tile);
 
 struct TnParams {
   const bf16* Y;   // [R][Hin]   layer input (A role: dW column index k)
   const bf16* dZ;  // [R][Hout]  layer pre-activation gradient (B role: dW row index o)
   int R, Hin, Hout;
   int splits;
+  int tile;        // 128 or 256 (tn_choose_tile); dw_reduce must be given the same value
   float* slab;     // [splits][Hout*Hin] fp32 in MFMA-native order (see dw_reduce)
 };
 
+int tn_choose_tile(int R, int Hin, int Hout);
 hipError_t gemm_tn_dw(const TnParams& p, hipStream_t s);
 // grad[o][k] (+)= sum_s slab[s]  (grad row-major [Hout][Hin])
-hipError_t dw_reduce(const float* slab, int splits, int Hin, int Hout, float* grad, int accumulate,
-                     hipStream_t s);
+hipError_t dw_reduce(const float* slab, int splits, int Hin, int Hout, int tile, float* grad,
+                     int accumulate, hipStream_t s);
 
 // elementwise / reduction kernels (elementwise.hip)
 hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, hipStream_t s);
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
-                     int R, int H, bf16* Y0, hipStream_t s);
+                     int R, int H, bf16* Y0, bf16* C0, hipStream_t s);
 hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_head, const float* y,
                      int n_valid, float gscale, float* out, float* g, float* sse_part,
                      float* gsum_part, hipStream_t s);

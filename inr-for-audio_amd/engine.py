@@ -85,7 +85,7 @@ class Workspace:
         e = lambda *s, dtype=f32: torch.empty(*s, dtype=dtype, device=device)  # noqa: E731
         self.rows = R
         self.Y = [e(R, H, dtype=bf) for _ in range(L + 1)]
-        self.C = [None] + [e(R, H, dtype=bf) for _ in range(L)]
+        self.C = [e(R, H, dtype=bf) for _ in range(L + 1)]
         self.out = e(R)
         self.g = torch.zeros(R, dtype=f32, device=device)
         self.head_part = e(H // 128, R)

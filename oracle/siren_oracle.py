@@ -135,7 +135,8 @@ def forward(p: Params, t: np.ndarray, omega0: float, omega: float, bf16: bool = 
     A0 = first_preact(t, p.W0, p.b0, omega0)
     Y0 = sin32(A0)
     Y = [bf16_round(Y0) if bf16 else Y0]
-    A, C = [A0], [None]
+    C0 = cos32(A0)
+    A, C = [A0], [bf16_round(C0) if bf16 else C0]
     for Wi, bi in zip(p.W, p.b):
         Wm = bf16_round(Wi) if bf16 else Wi
         z = np.asarray(Y[-1], dtype) @ np.asarray(Wm, dtype).T + np.asarray(bi, dtype)
@@ -178,7 +179,7 @@ def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float
         grads[f"net.{i}.linear.bias"] = db
         Wm = bf16_round(p.W[i - 1]) if bf16 else p.W[i - 1]
         dY = dZ @ np.asarray(Wm, dtype)
-    cos0 = np.cos(np.asarray(A[0], F64)).astype(dtype)
+    cos0 = np.asarray(C[0], dtype) if bf16 else np.cos(np.asarray(A[0], F64)).astype(dtype)
     dZ0 = dY * cos0 * dtype(omega0)
     tt = np.asarray(t, dtype).reshape(dZ0.shape[0], -1)
     grads["net.0.linear.weight"] = dZ0.T @ tt

@@ -38,7 +38,9 @@ def test_host_only_helpers(lib):
     assert lib.siren_abi_version() == 1
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
-    assert lib.siren_default_splits(1 << 20, 1024) == 16
+    assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256
+    assert lib.siren_dw_tile(44288, 256) == 128 and lib.siren_nt_tile(44160, 256) == 128
+    assert lib.siren_default_splits(1 << 20, 1024) == 32        # 16 tiles x 32 slices = 512 blocks
     assert lib.siren_default_splits(44160, 256) >= 1
     assert lib.siren_slab_floats(1024, 16) == 16 * 1024 * 1024
 
@@ -55,7 +57,7 @@ def test_validation_without_device(lib):
     assert lib.siren_inner_fwd(None, None, None, ctypes.c_float(30), 128, 256, None, None, None, None,
                                None) == 1002
     assert lib.siren_inner_bwd_dw(1, 1, 100, 256, 1, 1, None) == 1001    # rows % 64
-    assert lib.siren_first_fwd(1, 3, 1, 1, ctypes.c_float(1.0), 128, 256, 1, None) == 1003
+    assert lib.siren_first_fwd(1, 3, 1, 1, ctypes.c_float(1.0), 128, 256, 1, 1, None) == 1003
 
 
 @pytest.mark.parametrize("hidden", [128, 256, 512, 1024])

@@ -63,6 +63,31 @@ def test_train_step_grads_vs_oracle(dev, H, L, n, w0, in_dim, mb):
         assert np.array_equal(dev_p, pnew), k
 
 
+@pytest.mark.parametrize("tile", [128, 256])
+def test_train_step_forced_tiles(lib, dev, tile):
+    """The fused step with the NT and TN GEMM tile edge forced (256 is what the 2^20-coord
+    bench uses) against the oracle, SIREN 5x512 on 2048 rows."""
+    from inr_for_audio_amd.engine import SirenEngine
+    assert lib.siren_set_option(0, tile) == 0 and lib.siren_set_option(1, tile) == 0
+    try:
+        L, H, w0 = 4, 512, 3000.0
+        model = _model(H, L, w0)
+        sd0 = _sd(model)
+        t, y = _signal(2000)
+        eng = SirenEngine(model, t, y, device=dev)
+        eng.step()
+        torch.cuda.synchronize()
+    finally:
+        lib.siren_set_option(0, 0)
+        lib.siren_set_option(1, 0)
+    got = {k: v.detach().cpu().numpy() for k, v in zip(eng.layout.names, eng.grad_views())}
+    p = orc.Params.from_state_dict(sd0, L)
+    out, cache = orc.forward(p, t.numpy(), w0, 30.0, bf16=True, dtype=np.float64)
+    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), w0, 30.0, bf16=True)
+    for k, r in ref.items():
+        assert _rel(got[k].reshape(r.shape), r) < 2e-2, k
+
+
 def test_micro_batching_matches_full_batch(dev):
     from inr_for_audio_amd.engine import SirenEngine
     t, y = _signal(5000)

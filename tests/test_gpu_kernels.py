@@ -49,6 +49,19 @@ def _release():
     _KEEP.clear()
 
 
+@pytest.fixture(params=[128, 256])
+def nt_tile(request, lib):
+    """Force the NT GEMM tile edge (siren_set_option) for the duration of one test."""
+    ok(lib.siren_set_option(0, request.param), lib)
+    yield request.param
+    lib.siren_set_option(0, 0)
+
+
+def _skip_tile(tile, R, H):
+    if tile == 256 and (R % 256 or H % 256):
+        pytest.skip("256-tile needs rows and hidden multiples of 256")
+
+
 def bf16_np(t: torch.Tensor) -> np.ndarray:
     return t.float().cpu().numpy()
 
@@ -82,12 +95,13 @@ def test_first_fwd(lib, dev, in_dim, omega0):
     W0 = rng.uniform(-1, 1, (H, in_dim)).astype(F32)
     b0 = rng.uniform(-1, 1, H).astype(F32)
     Y0 = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    C0 = torch.empty_like(Y0)
     ok(lib.siren_first_fwd(ptr(to_dev(t, dev)), in_dim, ptr(to_dev(W0, dev)), ptr(to_dev(b0, dev)),
-                           ctypes.c_float(omega0), R, H, ptr(Y0), S()), lib)
-    ref = orc.sin32(orc.first_preact(t, W0, b0, omega0))  # fp32 restatement, correctly rounded sin
-    got = bf16_np(Y0)
-    assert within_bf16(got, ref, abs_slack=1e-6) <= 0
-    assert np.mean(got == orc.bf16_round(ref)) > 0.995
+                           ctypes.c_float(omega0), R, H, ptr(Y0), ptr(C0), S()), lib)
+    a0 = orc.first_preact(t, W0, b0, omega0)  # fp32 restatement (torch addmm rounding)
+    for got, ref in ((bf16_np(Y0), orc.sin32(a0)), (bf16_np(C0), orc.cos32(a0))):
+        assert within_bf16(got, ref, abs_slack=1e-6) <= 0
+        assert np.mean(got == orc.bf16_round(ref)) > 0.995
 
 
 def _inner_inputs(rng, R, H):
@@ -98,9 +112,10 @@ def _inner_inputs(rng, R, H):
     return X, W, b
 
 
-@pytest.mark.parametrize("R,H", [(256, 128), (512, 256), (384, 512), (256, 1024)])
+@pytest.mark.parametrize("R,H", [(256, 128), (512, 256), (384, 512), (256, 1024), (768, 512)])
 @pytest.mark.parametrize("head", [False, True])
-def test_inner_fwd(lib, dev, R, H, head):
+def test_inner_fwd(lib, dev, R, H, head, nt_tile):
+    _skip_tile(nt_tile, R, H)
     rng = np.random.default_rng(2)
     X, W, b = _inner_inputs(rng, R, H)
     Wb = orc.bf16_round(W)
@@ -162,15 +177,16 @@ def test_head_bwd(lib, dev, H):
                        atol=1e-9)
 
 
-@pytest.mark.parametrize("R,H", [(256, 128), (512, 256), (256, 1024)])
-def test_inner_bwd_dx(lib, dev, R, H):
+@pytest.mark.parametrize("R,H", [(256, 128), (512, 256), (256, 1024), (768, 512)])
+def test_inner_bwd_dx(lib, dev, R, H, nt_tile):
+    _skip_tile(nt_tile, R, H)
     rng = np.random.default_rng(5)
     dZ = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
     _, W, _ = _inner_inputs(rng, R, H)
     Wb = orc.bf16_round(W)
     Cp = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
     out = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
-    dbp = torch.empty(R // 128, H, device=dev)
+    dbp = torch.zeros(R // 128, H, device=dev)  # R / siren_nt_tile rows are written
     WT = np.ascontiguousarray(Wb.T)
     ok(lib.siren_inner_bwd_dx(ptr(to_dev(dZ, dev, torch.bfloat16)), ptr(to_dev(WT, dev, torch.bfloat16)),
                               ptr(to_dev(Cp, dev, torch.bfloat16)), ctypes.c_float(30.0), R, H, ptr(out),
@@ -184,7 +200,7 @@ def test_inner_bwd_dx(lib, dev, R, H):
 
 @pytest.mark.parametrize("in_dim", [1, 2])
 @pytest.mark.parametrize("omega0", [1000.0, 22000.0])
-def test_first_bwd_dx(lib, dev, in_dim, omega0):
+def test_first_bwd_dx(lib, dev, in_dim, omega0, nt_tile):
     rng = np.random.default_rng(6)
     R, H = 512, 256
     dZ1 = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
@@ -193,13 +209,14 @@ def test_first_bwd_dx(lib, dev, in_dim, omega0):
     t = rng.uniform(-1, 1, (R, in_dim)).astype(F32)
     W0 = rng.uniform(-1 / in_dim, 1 / in_dim, (H, in_dim)).astype(F32)
     b0 = rng.uniform(-1, 1, H).astype(F32)
-    part = torch.empty(R // 128, 1 + in_dim, H, device=dev)
+    part = torch.zeros(R // 128, 1 + in_dim, H, device=dev)
     WT = np.ascontiguousarray(Wb.T)
-    ok(lib.siren_first_bwd_dx(ptr(to_dev(dZ1, dev, torch.bfloat16)), ptr(to_dev(WT, dev, torch.bfloat16)),
-                              ptr(to_dev(t, dev)), in_dim, ptr(to_dev(W0, dev)), ptr(to_dev(b0, dev)),
-                              ctypes.c_float(omega0), R, H, ptr(part), S()), lib)
     A0 = orc.first_preact(t, W0, b0, omega0)
-    dz0 = (dZ1.astype(np.float64) @ Wb.astype(np.float64)) * np.cos(A0.astype(np.float64)) * omega0
+    C0 = orc.bf16_round(orc.cos32(A0))  # as siren_first_fwd stores it
+    ok(lib.siren_first_bwd_dx(ptr(to_dev(dZ1, dev, torch.bfloat16)), ptr(to_dev(WT, dev, torch.bfloat16)),
+                              ptr(to_dev(C0, dev, torch.bfloat16)), ptr(to_dev(t, dev)), in_dim,
+                              ctypes.c_float(omega0), R, H, ptr(part), S()), lib)
+    dz0 = (dZ1.astype(np.float64) @ Wb.astype(np.float64)) * C0 * omega0
     got = part.cpu().numpy().astype(np.float64).sum(0)
     ref_db = dz0.sum(0)
     scale = np.max(np.abs(dz0)) * math.sqrt(R)
@@ -209,17 +226,18 @@ def test_first_bwd_dx(lib, dev, in_dim, omega0):
         assert np.max(np.abs(got[1 + j] - ref_w)) < 1e-4 * scale
 
 
-@pytest.mark.parametrize("R,H,splits", [(256, 128, 1), (1024, 256, 3), (2048, 256, 16),
-                                        (512, 1024, 2), (640, 512, 5)])
-def test_inner_bwd_dw(lib, dev, R, H, splits):
+@pytest.mark.parametrize("R,H,splits,tile", [(256, 128, 1, 128), (1024, 256, 3, 128), (2048, 256, 16, 128),
+                                             (512, 1024, 2, 128), (640, 512, 5, 128), (1024, 256, 3, 256),
+                                             (2048, 512, 7, 256), (512, 1024, 2, 256), (320, 256, 9, 256)])
+def test_inner_bwd_dw(lib, dev, R, H, splits, tile):
     rng = np.random.default_rng(7)
     Y = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
     dZ = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
     slab = torch.empty(int(lib.siren_slab_floats(H, splits)), device=dev)
     grad = torch.full((H, H), 0.5, device=dev)
     ok(lib.siren_inner_bwd_dw(ptr(to_dev(Y, dev, torch.bfloat16)), ptr(to_dev(dZ, dev, torch.bfloat16)),
-                              R, H, splits, ptr(slab), S()), lib)
-    ok(lib.siren_dw_reduce(ptr(slab), splits, H, ptr(grad), 1, S()), lib)
+                              R, H, splits, tile, ptr(slab), S()), lib)
+    ok(lib.siren_dw_reduce(ptr(slab), splits, H, tile, ptr(grad), 1, S()), lib)
     ref = dZ.astype(np.float64).T @ Y.astype(np.float64) + 0.5
     got = grad.cpu().numpy().astype(np.float64)
     assert np.max(np.abs(got - ref)) < 1e-5 * np.max(np.abs(ref - 0.5)) + 1e-7

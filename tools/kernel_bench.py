@@ -1,0 +1,112 @@
+"""A/B timing of the individual SIREN kernels at the headline shape (2^20 coords x 1024)
+through the C-ABI, with HIP events, interleaved rounds in one process
+(cdna_hip_programming.md §5.4 rule 24).  Random bf16 data in realistic ranges.
+
+    python tools/kernel_bench.py [--rows 1048576] [--hidden 1024] [--rounds 5] [--reps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1 << 20)
+    ap.add_argument("--hidden", type=int, default=1024)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--tiles", default="128,256")
+    args = ap.parse_args()
+    import __graft_entry__ as ge
+    ge.build()
+    from inr_for_audio_amd import _lib
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    R, H = args.rows, args.hidden
+    s = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+    P = lambda t: t.data_ptr()  # noqa: E731
+    bf = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = (torch.rand(R, H, device=dev, generator=g) * 2 - 1).to(bf)
+    lim = math.sqrt(6 / H) / 30
+    W = ((torch.rand(H, H, device=dev, generator=g) * 2 - 1) * lim).to(bf)
+    WT = W.t().contiguous()
+    b = (torch.rand(H, device=dev, generator=g) - 0.5) * 0.06
+    hw = (torch.rand(H, device=dev, generator=g) - 0.5) * 0.02
+    Y = torch.empty(R, H, dtype=bf, device=dev)
+    C = torch.empty_like(Y)
+    dZ = (torch.randn(R, H, device=dev, generator=g) * 1e-3).to(bf)
+    dZp = torch.empty_like(Y)
+    hp = torch.empty(H // 128, R, device=dev)
+    part = torch.empty(R // 128, 3, H, device=dev)
+    t = torch.linspace(-1, 1, R, device=dev).reshape(R, 1)
+    W0 = torch.rand(H, 1, device=dev) * 2 - 1
+    b0 = torch.rand(H, device=dev) * 2 - 1
+    tiles = [int(x) for x in args.tiles.split(",")]
+    flops = 2.0 * R * H * H
+
+    def run_fwd():
+        return lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), None, None, s())
+
+    def run_fwd_head():
+        return lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), P(hw), P(hp), s())
+
+    def run_dx():
+        return lib.siren_inner_bwd_dx(P(dZ), P(WT), P(C), ctypes.c_float(30.0), R, H, P(dZp), P(part), s())
+
+    def run_dx0():
+        return lib.siren_first_bwd_dx(P(dZ), P(WT), P(C), P(t), 1, ctypes.c_float(3000.0), R, H, P(part), s())
+
+    def run_first():
+        return lib.siren_first_fwd(P(t), 1, P(W0), P(b0), ctypes.c_float(3000.0), R, H, P(Y), P(C), s())
+
+    slabs = {}
+
+    def run_dw(tile):
+        splits = lib.siren_default_splits(R, H) if tile == 0 else max(1, (512 if tile == 256 else 1024) // ((H // tile) ** 2))
+        if splits not in slabs:
+            slabs[splits] = torch.empty(int(lib.siren_slab_floats(H, splits)), device=dev)
+        return lib.siren_inner_bwd_dw(P(Y), P(dZ), R, H, splits, tile, P(slabs[splits]), s())
+
+    cases = {}
+    for tile in tiles:
+        cases[f"fwd_t{tile}"] = (tile, run_fwd, flops)
+        cases[f"fwd_head_t{tile}"] = (tile, run_fwd_head, flops)
+        cases[f"dx_t{tile}"] = (tile, run_dx, flops)
+        cases[f"dx0_t{tile}"] = (tile, run_dx0, flops)
+        cases[f"dw_t{tile}"] = (tile, (lambda tl=tile: run_dw(tl)), flops)
+    cases["first_fwd"] = (0, run_first, 0.0)
+    times = {k: [] for k in cases}
+    for _ in range(args.rounds):
+        for name, (tile, fn, _) in cases.items():
+            lib.siren_set_option(0, tile if not name.startswith("dw") else 0)
+            for _ in range(1):
+                _lib.check(fn(), name)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            for _ in range(args.reps):
+                fn()
+            ev1.record()
+            torch.cuda.synchronize()
+            times[name].append(ev0.elapsed_time(ev1) / args.reps)
+    lib.siren_set_option(0, 0)
+    out = {}
+    for name, (tile, fn, fl) in cases.items():
+        ts = sorted(times[name])
+        med = ts[len(ts) // 2]
+        out[name] = {"median_ms": med, "min_ms": ts[0], "tflops": (fl / (med * 1e-3) / 1e12) if fl else None}
+    print(json.dumps({"rows": R, "hidden": H, "results": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
