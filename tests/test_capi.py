@@ -56,7 +56,9 @@ def test_validation_without_device(lib):
     assert lib.siren_forward(ctypes.byref(net), ctypes.byref(SirenBatch()), None) == 1001
     assert lib.siren_inner_fwd(None, None, None, ctypes.c_float(30), 128, 256, None, None, None, None,
                                None) == 1002
-    assert lib.siren_inner_bwd_dw(1, 1, 100, 256, 1, 1, None) == 1001    # rows % 64
+    assert lib.siren_inner_bwd_dw(1, 1, 100, 256, 1, 0, 1, None) == 1001  # rows % 64
+    assert lib.siren_inner_bwd_dw(1, 1, 128, 256, 1, 64, 1, None) == 1003  # bad tile
+    assert lib.siren_dw_reduce(1, 1, 256, 0, 1, 1, None) == 1003           # tile must be explicit
     assert lib.siren_first_fwd(1, 3, 1, 1, ctypes.c_float(1.0), 128, 256, 1, 1, None) == 1003
 
 
