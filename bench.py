@@ -42,6 +42,36 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+KIND_MATCH = {  # profile kind -> substrings of the rocprofv3 kernel name
+    "inner_fwd": ("gemm_nt_kernel", ", 0, false>"),
+    "bwd_dx": ("gemm_nt_kernel", ", 1, false>"),
+    "bwd_dx0": ("gemm_nt_kernel", ", 2, false>"),
+    "bwd_dw": ("gemm_tn_kernel", ""),
+}
+
+
+def pmc_traffic(kind: str):
+    """Per-launch HBM bytes of `kind` from the newest committed PMC summary
+    (profiles/r*/bench_pmc_hbm.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate
+    passes).  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the
+    bytes of a 16-B/lane streaming read, so it is doubled; WRITE_SIZE is exact."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "bench_pmc_hbm.json")))
+    if not files or kind not in KIND_MATCH:
+        return None, None
+    with open(files[-1]) as f:
+        pmc = json.load(f)
+    a, b = KIND_MATCH[kind]
+
+    def avg(counter):
+        vals = [v["avg_KB_per_dispatch"] for k, v in pmc.get(counter, {}).items() if a in k and b in k]
+        return sum(vals) / len(vals) if vals else None
+    fetch, write = avg("FETCH_SIZE"), avg("WRITE_SIZE")
+    if fetch is None or write is None:
+        return None, None
+    return (2.0 * fetch + write) * 1024.0, os.path.relpath(files[-1], ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,6 +154,7 @@ def main():
     inner_flops_step = 6.0 * per_gpu * H * H * L
     gemm_ms_step = sum(kernels[k]["ms_per_step"] for k in gemm_kinds)
 
+    traffic, traffic_src = pmc_traffic(dom) if (H == 1024 and per_gpu == 1 << 20) else (None, None)
     ms_per_step = elapsed / args.steps * 1e3
     value = n_total * args.steps / elapsed
     result = {
@@ -136,8 +167,11 @@ def main():
                    "layers": args.layers, "omega0": args.omega0, "hidden_omega": 30.0,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": None,
-                     "flops_per_launch": flops_gemm},
+                     "unit": "TFLOP/s", "frac": achieved / PEAK_BF16_TFLOPS, "traffic": traffic,
+                     "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                     "flops_per_launch": flops_gemm,
+                     "hbm_gbs_at_traffic": (traffic / (kernels[dom]["avg_ms"] * 1e-3) / 1e9)
+                     if traffic else None},
         "step_mfma_frac": inner_flops_step / (ms_per_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS,
         "gemm_mfma_frac": inner_flops_step / (gemm_ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS,
         "kernels": kernels,
