@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tiles", default="128,256")
+    ap.add_argument("--only", default="", help="comma list of case-name prefixes to run")
     args = ap.parse_args()
     import __graft_entry__ as ge
     ge.build()
@@ -86,6 +87,9 @@ def main():
         cases[f"dx0_t{tile}"] = (tile, run_dx0, flops)
         cases[f"dw_t{tile}"] = (tile, (lambda tl=tile: run_dw(tl)), flops)
     cases["first_fwd"] = (0, run_first, 0.0)
+    if args.only:
+        pre = tuple(args.only.split(","))
+        cases = {k: v for k, v in cases.items() if k.startswith(pre)}
     times = {k: [] for k in cases}
     for _ in range(args.rounds):
         for name, (tile, fn, _) in cases.items():
