@@ -180,8 +180,12 @@ enum siren_prof_kind {
   SIREN_PROF_NKINDS = 8
 };
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
- * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge. */
-enum siren_option { SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1 };
+ * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;
+ * SIREN_OPT_NT_PIPE / SIREN_OPT_TN_PIPE = 0..2 selects the 256x256 K-loop variant
+ * (0: BK 64 double buffer, 1: BK 32 4-slot ring (default), 2: BK 32 5-slot ring). */
+enum siren_option {
+  SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1, SIREN_OPT_NT_PIPE = 2, SIREN_OPT_TN_PIPE = 3
+};
 int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);
 int siren_profile_reset(void);

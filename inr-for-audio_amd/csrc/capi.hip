@@ -384,10 +384,19 @@ int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wb,
 }
 
 int siren_set_option(int32_t option, int32_t value) {
-  if (value != 0 && value != 128 && value != 256) return SIREN_ERR_CONFIG;
   switch (option) {
-    case SIREN_OPT_NT_TILE: gemm_nt_set_tile(value); return SIREN_OK;
-    case SIREN_OPT_TN_TILE: gemm_tn_set_tile(value); return SIREN_OK;
+    case SIREN_OPT_NT_TILE:
+    case SIREN_OPT_TN_TILE:
+      if (value != 0 && value != 128 && value != 256) return SIREN_ERR_CONFIG;
+      if (option == SIREN_OPT_NT_TILE) gemm_nt_set_tile(value);
+      else gemm_tn_set_tile(value);
+      return SIREN_OK;
+    case SIREN_OPT_NT_PIPE:
+    case SIREN_OPT_TN_PIPE:
+      if (value < 0 || value > 2) return SIREN_ERR_CONFIG;
+      if (option == SIREN_OPT_NT_PIPE) gemm_nt_set_pipe(value);
+      else gemm_tn_set_pipe(value);
+      return SIREN_OK;
   }
   return SIREN_ERR_CONFIG;
 }

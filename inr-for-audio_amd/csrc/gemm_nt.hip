@@ -21,28 +21,47 @@
 // MFMA operand roles are swapped (A := W rows, B := X rows) so each lane ends up holding 4
 // consecutive output COLUMNS of one row: 8-byte contiguous bf16 stores, and per-row bias
 // loads as one float4.
+#include "gemm_pipeline.h"
 #include "siren_common.h"
 #include "siren_kernels.h"
 
 namespace siren {
 
-template <int BM_, int BN_, int WM_, int WN_>
+// Source-side XOR swizzle of a staged [rows][BK] bf16 image (16-B chunks).  BK = 64 (128-B
+// rows, 8 chunks): chunk ^ (row & 7).  BK = 32 (64-B rows, 4 chunks): chunk ^ H[(row>>2)&3]
+// with H = {0,2,3,1}, which makes every 16-lane group of a ds_read_b128 fragment read hit 16
+// distinct 16-B bank slots.
+template <int BK>
+__device__ __forceinline__ int stage_swz(int r, int c) {
+  if constexpr (BK == 64) return c ^ (r & 7);
+  else return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3);  // H = {0,2,3,1} as 2-bit fields of 0x78
+}
+
+template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_, bool FP_>
 struct NtCfg {
-  static constexpr int BM = BM_, BN = BN_, BK = 64;
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, S = S_;
+  static constexpr bool FP = FP_;
   static constexpr int WM = WM_, WN = WN_, NWAVES = WM_ * WN_, THREADS = 64 * NWAVES;
   static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   static constexpr int SM = TM / 16, SN = TN / 16;  // 16x16 MFMA tiles per wave
-  static constexpr int XBYTES = BM * BK * 2, WBYTES = BN * BK * 2;
+  static constexpr int ROWB = BK * 2;               // bytes per staged row
+  static constexpr int XBYTES = BM * ROWB, WBYTES = BN * ROWB;
   static constexpr int STAGE = XBYTES + WBYTES;
-  static constexpr int LDS = 2 * STAGE;
+  static constexpr int LDS = S * STAGE;
   static constexpr int XINSTR = XBYTES / 1024 / NWAVES;  // LDS-DMA instructions per wave per stage
   static constexpr int WINSTR = WBYTES / 1024 / NWAVES;
   static constexpr int RED_STRIDE = BN + 4;
   static_assert(XBYTES % (1024 * NWAVES) == 0 && WBYTES % (1024 * NWAVES) == 0, "staging split");
   static_assert(WM * 16 * RED_STRIDE * 4 <= LDS && WN * BM * 4 <= LDS, "epilogue scratch");
+  static_assert(LDS <= 160 * 1024, "LDS");
 };
-using NtSmall = NtCfg<128, 128, 2, 2>;
-using NtLarge = NtCfg<256, 256, 2, 4>;
+using NtSmall = NtCfg<128, 128, 2, 2, 64, 2, false>;
+// 256x256 variants, selected by siren_set_option(SIREN_OPT_PIPE, v) for A/B measurement
+using NtL0 = NtCfg<256, 256, 2, 4, 64, 2, false>;  // BK 64, double buffer
+using NtL1 = NtCfg<256, 256, 2, 4, 32, 4, false>;  // BK 32, 4-slot ring (3 steps ahead)
+using NtL2 = NtCfg<256, 256, 2, 4, 32, 5, false>;  // BK 32, 5-slot ring
+// (fragment prefetch across the barrier, FP = true, needs a second 48-VGPR fragment set on
+//  top of 128 accumulators and spills at this tile: not instantiated)
 
 template <class Cfg, int MODE, bool HEAD>
 __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
@@ -62,33 +81,38 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- LDS-DMA staging addresses -------------------------------------------------
-  // One instruction moves 8 rows x 128 B.  Lane L lands at LDS row r = L>>3, 16-B slot
-  // s = L&7 and carries the logical 16-B chunk c = s ^ (r & 7) (source-side swizzle).
-  const int srow = lane >> 3;
-  const int schunk = (lane & 7) ^ srow;
-  const bf16* xg = p.X + (size_t)(m0 + wave * Cfg::XINSTR * 8 + srow) * K + schunk * 8;
-  const bf16* wg = p.W + (size_t)(n0 + wave * Cfg::WINSTR * 8 + srow) * K + schunk * 8;
-  const size_t row8 = (size_t)8 * K;
-
-  auto stage = [&](int kt, int buf) {
-    char* xs = smem + buf * Cfg::STAGE + wave * Cfg::XINSTR * 1024;
-    char* ws = smem + buf * Cfg::STAGE + Cfg::XBYTES + wave * Cfg::WINSTR * 1024;
-    const bf16* xk = xg + kt * BK;
-    const bf16* wk = wg + kt * BK;
+  // One instruction moves 1 KiB = RPI rows x ROWB bytes.  Lane L lands at row L/SPR, 16-B
+  // slot L%SPR, and carries the logical chunk stage_swz(row, slot) (source-side swizzle).
+  constexpr int ROWB = Cfg::ROWB, RPI = 1024 / ROWB, SPR = ROWB / 16;
+  size_t xoff[Cfg::XINSTR], woff[Cfg::WINSTR];
 #pragma unroll
-    for (int j = 0; j < Cfg::XINSTR; ++j) glds16(xk + j * row8, lds_ptr(xs + j * 1024));
+  for (int j = 0; j < Cfg::XINSTR; ++j) {
+    const int r = (wave * Cfg::XINSTR + j) * RPI + lane / SPR;
+    xoff[j] = (size_t)(m0 + r) * K + stage_swz<BK>(r, lane % SPR) * 8;
+  }
 #pragma unroll
-    for (int j = 0; j < Cfg::WINSTR; ++j) glds16(wk + j * row8, lds_ptr(ws + j * 1024));
+  for (int j = 0; j < Cfg::WINSTR; ++j) {
+    const int r = (wave * Cfg::WINSTR + j) * RPI + lane / SPR;
+    woff[j] = (size_t)(n0 + r) * K + stage_swz<BK>(r, lane % SPR) * 8;
+  }
+  auto stage = [&](int kt, int slot) {
+    char* xs = smem + slot * Cfg::STAGE + wave * Cfg::XINSTR * 1024;
+    char* ws = smem + slot * Cfg::STAGE + Cfg::XBYTES + wave * Cfg::WINSTR * 1024;
+    const bf16* xk = p.X + kt * BK;
+    const bf16* wk = p.W + kt * BK;
+#pragma unroll
+    for (int j = 0; j < Cfg::XINSTR; ++j) glds16(xk + xoff[j], lds_ptr(xs + j * 1024));
+#pragma unroll
+    for (int j = 0; j < Cfg::WINSTR; ++j) glds16(wk + woff[j], lds_ptr(ws + j * 1024));
   };
 
   // ---- fragment read offsets --------------------------------------------------------
-  // 16x16x32 operand: lane holds row (lane&15), k = 8*(lane>>4) .. +7 of a 32-deep half.
-  // Physical slot of logical chunk c in row r is c ^ (r&7); r&7 == lane&7 here.
-  const int frow = lane & 15;
-  int koff[2];
+  // 16x16x32 operand: lane holds row (lane&15), k = 8*(lane>>4) .. +7 of a 32-deep half;
+  // the fragment's rows start at multiples of 16, so the swizzle depends on the lane only.
+  int koff[BK / 32];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-    koff[kk] = frow * 128 + ((((lane >> 4) + 4 * kk) ^ (lane & 7)) << 4);
+  for (int kk = 0; kk < BK / 32; ++kk)
+    koff[kk] = (lane & 15) * ROWB + (stage_swz<BK>(lane & 15, (lane >> 4) + 4 * kk) << 4);
 
   f32x4 acc[SN][SM];
 #pragma unroll
@@ -96,36 +120,15 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
     for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    const char* xs = smem + cur * Cfg::STAGE;
+  auto frags = [&](int slot, int kk, bf16x8 (&A)[SN], bf16x8 (&B)[SM]) {
+    const char* xs = smem + slot * Cfg::STAGE;
     const char* ws = xs + Cfg::XBYTES;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[SN], bfm[SM];
+    for (int i = 0; i < SN; ++i) A[i] = *(const bf16x8*)(ws + (wn * TN + i * 16) * ROWB + koff[kk]);
 #pragma unroll
-      for (int i = 0; i < SN; ++i)
-        af[i] = *(const bf16x8*)(ws + (wn * TN + i * 16) * 128 + koff[kk]);
-#pragma unroll
-      for (int j = 0; j < SM; ++j)
-        bfm[j] = *(const bf16x8*)(xs + (wm * TM + j * 16) * 128 + koff[kk]);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < SN; ++i)
-#pragma unroll
-        for (int j = 0; j < SM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfm[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
+    for (int j = 0; j < SM; ++j) B[j] = *(const bf16x8*)(xs + (wm * TM + j * 16) * ROWB + koff[kk]);
+  };
+  mfma_pipeline<Cfg::S, Cfg::FP, BK / 32, Cfg::XINSTR + Cfg::WINSTR>(K / BK, acc, stage, frags);
 
   // ---- epilogue ------------------------------------------------------------------
   // acc[i][j][r] = out[m][n] with m = m0 + wm*TM + j*16 + (lane&15),
@@ -266,22 +269,29 @@ static hipError_t dispatch_mode(int mode, bool head, const NtParams& p, hipStrea
 
 // tile override for A/B measurement: 0 = auto, 128 or 256
 static int g_nt_tile = 0;
+static int g_nt_pipe = 1;  // default 256x256 pipeline variant (see NtL*)
 void gemm_nt_set_tile(int tile) { g_nt_tile = tile; }
+void gemm_nt_set_pipe(int v) { g_nt_pipe = v; }
 
 int nt_choose_tile(int M, int N) {
-  const bool large_ok = (M % NtLarge::BM == 0) && (N % NtLarge::BN == 0);
+  const bool large_ok = (M % 256 == 0) && (N % 256 == 0);
   if (g_nt_tile == 128 || !large_ok) return 128;
   if (g_nt_tile == 256) return 256;
   // the 256x256 tile (1 block/CU) needs >= 2 blocks per CU to keep 256 CUs busy
-  return (long)(M / NtLarge::BM) * (N / NtLarge::BN) >= 512 ? 256 : 128;
+  return (long)(M / 256) * (N / 256) >= 512 ? 256 : 128;
 }
 
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (p.M % NtSmall::BM || p.N % NtSmall::BN || p.K % NtSmall::BK || p.M <= 0) return hipErrorInvalidValue;
   if (mode == NT_DX0 && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
   if (p.tile == 256) {
-    if (p.M % NtLarge::BM || p.N % NtLarge::BN) return hipErrorInvalidValue;
-    return dispatch_mode<NtLarge>(mode, head, p, s);
+    if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
+    switch (g_nt_pipe) {
+      case 0: return dispatch_mode<NtL0>(mode, head, p, s);
+      case 1: return dispatch_mode<NtL1>(mode, head, p, s);
+      case 2: return dispatch_mode<NtL2>(mode, head, p, s);
+    }
+    return hipErrorInvalidValue;
   }
   if (p.tile != 128) return hipErrorInvalidValue;
   return dispatch_mode<NtSmall>(mode, head, p, s);

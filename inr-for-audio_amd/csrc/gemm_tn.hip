@@ -13,25 +13,30 @@
 // instruction).  dw_reduce sums the slices in a fixed order (deterministic).
 // Tiles: 128x128 / 4 waves (small grids) or 256x256 / 8 waves (half the LDS-fill bytes per
 // flop); the choice is made once per call by tn_choose_tile and passed to both kernels.
+#include "gemm_pipeline.h"
 #include "siren_common.h"
 #include "siren_kernels.h"
 
 namespace siren {
 
-template <int BI_, int BJ_, int WM_, int WN_>
+template <int BI_, int BJ_, int WM_, int WN_, int BK_ = 64, int S_ = 2>
 struct TnCfg {
-  static constexpr int BI = BI_, BJ = BJ_, BK = 64;
+  static constexpr int BI = BI_, BJ = BJ_, BK = BK_, S = S_;
   static constexpr int WM = WM_, WN = WN_, NWAVES = WM_ * WN_, THREADS = 64 * NWAVES;
   static constexpr int TI = BI / WM, TJ = BJ / WN, SI = TI / 16, SJ = TJ / 16;
   static constexpr int YROW = BI * 2, ZROW = BJ * 2;       // bytes per staged row
   static constexpr int YBYTES = BK * YROW, ZBYTES = BK * ZROW;
-  static constexpr int STAGE = YBYTES + ZBYTES, LDS = 2 * STAGE;
+  static constexpr int STAGE = YBYTES + ZBYTES, LDS = S * STAGE;
   static constexpr int YINSTR = YBYTES / 1024 / NWAVES, ZINSTR = ZBYTES / 1024 / NWAVES;
   static constexpr int TILE_FLOATS = BI * BJ;
   static_assert(YBYTES % (1024 * NWAVES) == 0 && ZBYTES % (1024 * NWAVES) == 0, "staging split");
+  static_assert(LDS <= 160 * 1024, "LDS");
 };
 using TnSmall = TnCfg<128, 128, 2, 2>;
-using TnLarge = TnCfg<256, 256, 2, 4>;
+using TnLarge = TnCfg<256, 256, 2, 4>;          // slab geometry of every 256x256 variant
+using TnL0 = TnCfg<256, 256, 2, 4, 64, 2>;      // BK 64, double buffer
+using TnL1 = TnCfg<256, 256, 2, 4, 32, 4>;      // BK 32, 4-slot ring
+using TnL2 = TnCfg<256, 256, 2, 4, 32, 5>;      // BK 32, 5-slot ring
 
 // Chunk swizzle of a staged [64][cols] image: physical 16-B chunk = c ^ f(r).  With
 // h(r) = (r&3) | ((r>>3)&1)<<2 and f = 2h, the 8 rows a 32-lane half touches in one
@@ -84,7 +89,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
     const int r = (wave * Cfg::ZINSTR + j) * RPI + lane / SPR;
     zoff[j] = (size_t)r * p.Hout + o0 + (((lane % SPR) ^ tn_swz(r)) * 8);
   }
-  auto stage = [&](int ks, int buf) {
+  auto stage = [&](int kt, int buf) {
+    const int ks = ks_begin + kt;
     char* ys = smem + buf * Cfg::STAGE + wave * Cfg::YINSTR * 1024;
     char* zs = smem + buf * Cfg::STAGE + Cfg::YBYTES + wave * Cfg::ZINSTR * 1024;
     const bf16* yb = p.Y + (size_t)ks * BK * p.Hin;
@@ -115,34 +121,15 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
 #pragma unroll
     for (int j = 0; j < SJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (ks_begin < ks_end) {
-    stage(ks_begin, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int ks = ks_begin; ks < ks_end; ++ks) {
-      const int cur = (ks - ks_begin) & 1;
-      if (ks + 1 < ks_end) stage(ks + 1, cur ^ 1);
-      const char* ys = smem + cur * Cfg::STAGE;
-      const char* zs = ys + Cfg::YBYTES;
+  auto frags = [&](int slot, int kk, bf16x8 (&A)[SI], bf16x8 (&B)[SJ]) {
+    const char* ys = smem + slot * Cfg::STAGE;
+    const char* zs = ys + Cfg::YBYTES;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 af[SI], bfz[SJ];
+    for (int s = 0; s < SI; ++s) A[s] = tr_frag<YROW>(ys + kk * 32 * YROW + colA[s]);
 #pragma unroll
-        for (int s = 0; s < SI; ++s) af[s] = tr_frag<YROW>(ys + kk * 32 * YROW + colA[s]);
-#pragma unroll
-        for (int s = 0; s < SJ; ++s) bfz[s] = tr_frag<ZROW>(zs + kk * 32 * ZROW + colB[s]);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < SI; ++i)
-#pragma unroll
-          for (int j = 0; j < SJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfz[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  }
+    for (int s = 0; s < SJ; ++s) B[s] = tr_frag<ZROW>(zs + kk * 32 * ZROW + colB[s]);
+  };
+  mfma_pipeline<Cfg::S, false, BK / 32, Cfg::YINSTR + Cfg::ZINSTR>(ks_end - ks_begin, acc, stage, frags);
 
   // native-order slab store: [slice][tile][wave][i*SJ+j][lane] float4
   float4* dst = (float4*)(p.slab + ((size_t)slice * ntile + tile) * Cfg::TILE_FLOATS) +
@@ -155,7 +142,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
 }
 
 static int g_tn_tile = 0;
+static int g_tn_pipe = 1;
 void gemm_tn_set_tile(int tile) { g_tn_tile = tile; }
+void gemm_tn_set_pipe(int v) { g_tn_pipe = v; }
 
 int tn_choose_tile(int R, int Hin, int Hout) {
   const bool large_ok = (Hin % 256 == 0) && (Hout % 256 == 0);
@@ -177,7 +166,12 @@ hipError_t gemm_tn_dw(const TnParams& p, hipStream_t s) {
   if (p.Hin % 128 || p.Hout % 128 || p.R % 64 || p.R <= 0 || p.splits < 1) return hipErrorInvalidValue;
   if (p.tile == 256) {
     if (p.Hin % 256 || p.Hout % 256) return hipErrorInvalidValue;
-    return launch_tn<TnLarge>(p, s);
+    switch (g_tn_pipe) {
+      case 0: return launch_tn<TnL0>(p, s);
+      case 1: return (p.R % 32) ? hipErrorInvalidValue : launch_tn<TnL1>(p, s);
+      case 2: return launch_tn<TnL2>(p, s);
+    }
+    return hipErrorInvalidValue;
   }
   if (p.tile != 128) return hipErrorInvalidValue;
   return launch_tn<TnSmall>(p, s);

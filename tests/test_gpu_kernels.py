@@ -49,12 +49,23 @@ def _release():
     _KEEP.clear()
 
 
-@pytest.fixture(params=[128, 256])
+@pytest.fixture(params=[(128, 0), (256, 0), (256, 1), (256, 2)], ids=lambda p: f"t{p[0]}p{p[1]}")
 def nt_tile(request, lib):
-    """Force the NT GEMM tile edge (siren_set_option) for the duration of one test."""
-    ok(lib.siren_set_option(0, request.param), lib)
-    yield request.param
+    """Force the NT GEMM tile edge and 256x256 K-loop variant (siren_set_option) for the
+    duration of one test."""
+    tile, pipe = request.param
+    ok(lib.siren_set_option(0, tile), lib)
+    ok(lib.siren_set_option(2, pipe), lib)
+    yield tile
     lib.siren_set_option(0, 0)
+    lib.siren_set_option(2, 1)
+
+
+@pytest.fixture(params=[0, 1, 2], ids=lambda p: f"p{p}")
+def tn_pipe(request, lib):
+    ok(lib.siren_set_option(3, request.param), lib)
+    yield request.param
+    lib.siren_set_option(3, 1)
 
 
 def _skip_tile(tile, R, H):
@@ -229,7 +240,9 @@ def test_first_bwd_dx(lib, dev, in_dim, omega0, nt_tile):
 @pytest.mark.parametrize("R,H,splits,tile", [(256, 128, 1, 128), (1024, 256, 3, 128), (2048, 256, 16, 128),
                                              (512, 1024, 2, 128), (640, 512, 5, 128), (1024, 256, 3, 256),
                                              (2048, 512, 7, 256), (512, 1024, 2, 256), (320, 256, 9, 256)])
-def test_inner_bwd_dw(lib, dev, R, H, splits, tile):
+def test_inner_bwd_dw(lib, dev, R, H, splits, tile, tn_pipe):
+    if tile == 128 and tn_pipe != 1:
+        pytest.skip("pipeline variants apply to the 256x256 tile")
     rng = np.random.default_rng(7)
     Y = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
     dZ = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tiles", default="128,256")
+    ap.add_argument("--pipes", default="0,1,2", help="256x256 K-loop variants to time")
     ap.add_argument("--only", default="", help="comma list of case-name prefixes to run")
     args = ap.parse_args()
     import __graft_entry__ as ge
@@ -80,20 +81,25 @@ def main():
         return lib.siren_inner_bwd_dw(P(Y), P(dZ), R, H, splits, tile, P(slabs[splits]), s())
 
     cases = {}
+    pipes = [int(x) for x in args.pipes.split(",")]
     for tile in tiles:
-        cases[f"fwd_t{tile}"] = (tile, run_fwd, flops)
-        cases[f"fwd_head_t{tile}"] = (tile, run_fwd_head, flops)
-        cases[f"dx_t{tile}"] = (tile, run_dx, flops)
-        cases[f"dx0_t{tile}"] = (tile, run_dx0, flops)
-        cases[f"dw_t{tile}"] = (tile, (lambda tl=tile: run_dw(tl)), flops)
-    cases["first_fwd"] = (0, run_first, 0.0)
+        for pipe in (pipes if tile == 256 else [0]):
+            sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "")
+            cases[f"fwd_{sfx}"] = (tile, pipe, run_fwd, flops)
+            cases[f"fwd_head_{sfx}"] = (tile, pipe, run_fwd_head, flops)
+            cases[f"dx_{sfx}"] = (tile, pipe, run_dx, flops)
+            cases[f"dx0_{sfx}"] = (tile, pipe, run_dx0, flops)
+            cases[f"dw_{sfx}"] = (tile, pipe, (lambda tl=tile: run_dw(tl)), flops)
+    cases["first_fwd"] = (0, 1, run_first, 0.0)
     if args.only:
         pre = tuple(args.only.split(","))
         cases = {k: v for k, v in cases.items() if k.startswith(pre)}
     times = {k: [] for k in cases}
     for _ in range(args.rounds):
-        for name, (tile, fn, _) in cases.items():
+        for name, (tile, pipe, fn, _) in cases.items():
             lib.siren_set_option(0, tile if not name.startswith("dw") else 0)
+            lib.siren_set_option(2, pipe)
+            lib.siren_set_option(3, pipe)
             for _ in range(1):
                 _lib.check(fn(), name)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -104,8 +110,10 @@ def main():
             torch.cuda.synchronize()
             times[name].append(ev0.elapsed_time(ev1) / args.reps)
     lib.siren_set_option(0, 0)
+    lib.siren_set_option(2, 1)
+    lib.siren_set_option(3, 1)
     out = {}
-    for name, (tile, fn, fl) in cases.items():
+    for name, (tile, pipe, fn, fl) in cases.items():
         ts = sorted(times[name])
         med = ts[len(ts) // 2]
         out[name] = {"median_ms": med, "min_ms": ts[0], "tflops": (fl / (med * 1e-3) / 1e12) if fl else None}
