@@ -101,9 +101,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     const bf16* xk = p.X + kt * BK;
     const bf16* wk = p.W + kt * BK;
 #pragma unroll
-    for (int j = 0; j < Cfg::XINSTR; ++j) glds16(xk + xoff[j], lds_ptr(xs + j * 1024));
+    for (int j = 0; j < Cfg::XINSTR; ++j) glds16_asm(xk + xoff[j], lds_addr(xs + j * 1024));
 #pragma unroll
-    for (int j = 0; j < Cfg::WINSTR; ++j) glds16(wk + woff[j], lds_ptr(ws + j * 1024));
+    for (int j = 0; j < Cfg::WINSTR; ++j) glds16_asm(wk + woff[j], lds_addr(ws + j * 1024));
   };
 
   // ---- fragment read offsets --------------------------------------------------------

@@ -96,9 +96,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
     const bf16* yb = p.Y + (size_t)ks * BK * p.Hin;
     const bf16* zb = p.dZ + (size_t)ks * BK * p.Hout;
 #pragma unroll
-    for (int j = 0; j < Cfg::YINSTR; ++j) glds16(yb + yoff[j], lds_ptr(ys + j * 1024));
+    for (int j = 0; j < Cfg::YINSTR; ++j) glds16_asm(yb + yoff[j], lds_addr(ys + j * 1024));
 #pragma unroll
-    for (int j = 0; j < Cfg::ZINSTR; ++j) glds16(zb + zoff[j], lds_ptr(zs + j * 1024));
+    for (int j = 0; j < Cfg::ZINSTR; ++j) glds16_asm(zb + zoff[j], lds_addr(zs + j * 1024));
   };
 
   // transposed-read addresses: group g = lane>>4, lane-in-group 4q+p supplies row q (+4 for

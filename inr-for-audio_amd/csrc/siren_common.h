@@ -38,6 +38,29 @@ __device__ __forceinline__ LDS_AS void* lds_ptr(char* p) {
   return (LDS_AS void*)(p);
 }
 
+// LDS-DMA issued from inline asm: hipcc's waitcnt pass cannot see it, so it does NOT insert
+// the conservative `s_waitcnt vmcnt(0)` before every later ds_read of the same __shared__
+// array (it cannot prove the DMA targets another ring slot).  The caller orders the data
+// with its own counted vmcnt + barrier (gemm_pipeline.h).  M0 is compiler-reserved, so it
+// is saved and restored inside the one statement (cdna_hip_programming.md §5.7 item M0).
+// `lds_byte` must be wave-uniform.
+__device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte))
+      : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return (unsigned)(uintptr_t)(const LDS_AS char*)(p);
+}
+
 __device__ __forceinline__ bf16x4 pack4(float a, float b, float c, float d) {
   bf16x4 r;
   r[0] = (bf16)a; r[1] = (bf16)b; r[2] = (bf16)c; r[3] = (bf16)d;
