@@ -181,10 +181,14 @@ enum siren_prof_kind {
 };
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
  * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;
- * SIREN_OPT_NT_PIPE / SIREN_OPT_TN_PIPE = 0..2 selects the 256x256 K-loop variant
- * (0: BK 64 double buffer, 1: BK 32 4-slot ring (default), 2: BK 32 5-slot ring). */
+ * SIREN_OPT_NT_PIPE = 1 persistent 256x256 NT GEMM (default) / 0 one tile per block;
+ * SIREN_OPT_TN_PIPE = 0..2 selects the 256x256 dW K-loop (0: BK 64 double buffer
+ * (default), 1: BK 32 4-slot ring, 2: BK 32 5-slot ring);
+ * SIREN_OPT_NT_GRID = persistent NT grid size (0 = one block per CU; tests use small
+ * values so every block walks several tiles). */
 enum siren_option {
-  SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1, SIREN_OPT_NT_PIPE = 2, SIREN_OPT_TN_PIPE = 3
+  SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1, SIREN_OPT_NT_PIPE = 2, SIREN_OPT_TN_PIPE = 3,
+  SIREN_OPT_NT_GRID = 4
 };
 int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);

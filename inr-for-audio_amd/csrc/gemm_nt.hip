@@ -11,12 +11,14 @@
 //            column partial sums of dz and dz*t_j (db0, dW0) are written; dZ0 never
 //            reaches HBM.
 //
-// Two tile configurations (NtCfg): 128x128 with 4 waves (2 blocks/CU, used when the grid
-// is small) and 256x256 with 8 waves (1 block/CU, half the L2->LDS bytes per flop).  Each
-// wave owns a (BM/WM) x (BN/WN) sub-tile of v_mfma_f32_16x16x32_bf16 tiles.  Operands are
-// staged HBM->LDS by LDS-DMA (global_load_lds_dwordx4), double-buffered, with an XOR
-// swizzle applied on the SOURCE address so that the ds_read_b128 fragment reads are
-// bank-conflict free (cdna_hip_programming.md §5.4 rule 21 / T2).
+// Tiles: 256x256 with 8 waves (2x4, each 128x64 = 8x4 v_mfma_f32_16x16x32_bf16 tiles),
+// PERSISTENT: one block per CU walks its tiles and the double-buffered LDS ring runs across
+// tile boundaries (gemm_pipeline.h mfma_pipeline_tiles), so tile i+1's first operand stage
+// is loading while tile i's epilogue runs and the epilogue's stores drain under tile i+1's
+// MFMAs.  A 128x128 / 4-wave config (2 blocks per CU, one tile per block) serves grids too
+// small for 256x256.  Operands are staged HBM->LDS by LDS-DMA (global_load_lds_dwordx4 from
+// inline asm), with an XOR swizzle on the SOURCE address so that the ds_read_b128 fragment
+// reads are bank-conflict free (cdna_hip_programming.md §5.4 rule 21 / T2).
 //
 // MFMA operand roles are swapped (A := W rows, B := X rows) so each lane ends up holding 4
 // consecutive output COLUMNS of one row: 8-byte contiguous bf16 stores, and per-row bias
@@ -27,41 +29,34 @@
 
 namespace siren {
 
-// Source-side XOR swizzle of a staged [rows][BK] bf16 image (16-B chunks).  BK = 64 (128-B
-// rows, 8 chunks): chunk ^ (row & 7).  BK = 32 (64-B rows, 4 chunks): chunk ^ H[(row>>2)&3]
-// with H = {0,2,3,1}, which makes every 16-lane group of a ds_read_b128 fragment read hit 16
-// distinct 16-B bank slots.
-template <int BK>
-__device__ __forceinline__ int stage_swz(int r, int c) {
-  if constexpr (BK == 64) return c ^ (r & 7);
-  else return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3);  // H = {0,2,3,1} as 2-bit fields of 0x78
-}
+// Source-side XOR swizzle of a staged [rows][64] bf16 image (128-B rows, 8 16-B chunks).
+__device__ __forceinline__ int stage_swz(int r, int c) { return c ^ (r & 7); }
 
-template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_, bool FP_>
+template <int BM_, int BN_, int WM_, int WN_>
 struct NtCfg {
-  static constexpr int BM = BM_, BN = BN_, BK = BK_, S = S_;
-  static constexpr bool FP = FP_;
+  static constexpr int BM = BM_, BN = BN_, BK = 64;
   static constexpr int WM = WM_, WN = WN_, NWAVES = WM_ * WN_, THREADS = 64 * NWAVES;
   static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   static constexpr int SM = TM / 16, SN = TN / 16;  // 16x16 MFMA tiles per wave
   static constexpr int ROWB = BK * 2;               // bytes per staged row
   static constexpr int XBYTES = BM * ROWB, WBYTES = BN * ROWB;
   static constexpr int STAGE = XBYTES + WBYTES;
-  static constexpr int LDS = S * STAGE;
+  static constexpr int LDS = 2 * STAGE;
   static constexpr int XINSTR = XBYTES / 1024 / NWAVES;  // LDS-DMA instructions per wave per stage
   static constexpr int WINSTR = WBYTES / 1024 / NWAVES;
   static constexpr int RED_STRIDE = BN + 4;
   static_assert(XBYTES % (1024 * NWAVES) == 0 && WBYTES % (1024 * NWAVES) == 0, "staging split");
-  static_assert(WM * 16 * RED_STRIDE * 4 <= LDS && WN * BM * 4 <= LDS, "epilogue scratch");
-  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(WM * 16 * RED_STRIDE * 4 <= STAGE && WN * BM * 4 <= STAGE, "epilogue scratch in one slot");
 };
-using NtSmall = NtCfg<128, 128, 2, 2, 64, 2, false>;
-// 256x256 variants, selected by siren_set_option(SIREN_OPT_PIPE, v) for A/B measurement
-using NtL0 = NtCfg<256, 256, 2, 4, 64, 2, false>;  // BK 64, double buffer
-using NtL1 = NtCfg<256, 256, 2, 4, 32, 4, false>;  // BK 32, 4-slot ring (3 steps ahead)
-using NtL2 = NtCfg<256, 256, 2, 4, 32, 5, false>;  // BK 32, 5-slot ring
-// (fragment prefetch across the barrier, FP = true, needs a second 48-VGPR fragment set on
-//  top of 128 accumulators and spills at this tile: not instantiated)
+using NtSmall = NtCfg<128, 128, 2, 2>;
+using NtLarge = NtCfg<256, 256, 2, 4>;
+
+// store instructions an epilogue issues per wave (lower bound; see mfma_pipeline_tiles)
+template <class Cfg, int MODE>
+constexpr int epilogue_stores() {
+  return MODE == NT_FWD ? (2 * Cfg::SM * Cfg::SN > 63 ? 63 : 2 * Cfg::SM * Cfg::SN)
+                        : (MODE == NT_DX ? Cfg::SM * Cfg::SN : 0);
+}
 
 template <class Cfg, int MODE, bool HEAD>
 __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
@@ -76,50 +71,54 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   const int wm = wave / WN, wn = wave % WN;
   const int K = p.K, N = p.N;
   const int tiles_n = N / BN;
-  const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = g / tiles_n, tn = g - tm * tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int ntiles = (p.M / BM) * tiles_n;
+  // Block b takes tiles b', b'+G, ... with b' the XCD-grouped id: the G/8 blocks of one XCD
+  // hold consecutive tile ids, i.e. they share X row-blocks in L2 at the same time.
+  const int G = gridDim.x;
+  const int bp = xcd_remap(blockIdx.x, G);
+  const int my_tiles = (ntiles - bp + G - 1) / G;
+  auto tile_of = [&](int i, int& m0, int& n0) {
+    const int g = bp + i * G;
+    const int tm = g / tiles_n;
+    m0 = tm * BM;
+    n0 = (g - tm * tiles_n) * BN;
+  };
 
   // ---- LDS-DMA staging addresses -------------------------------------------------
-  // One instruction moves 1 KiB = RPI rows x ROWB bytes.  Lane L lands at row L/SPR, 16-B
-  // slot L%SPR, and carries the logical chunk stage_swz(row, slot) (source-side swizzle).
-  constexpr int ROWB = Cfg::ROWB, RPI = 1024 / ROWB, SPR = ROWB / 16;
-  size_t xoff[Cfg::XINSTR], woff[Cfg::WINSTR];
+  // One instruction moves 8 rows x 128 B.  Lane L lands at row L/8, 16-B slot L%8, and
+  // carries the logical chunk stage_swz(row, slot) (source-side swizzle).
+  constexpr int ROWB = Cfg::ROWB;
+  size_t xrel[Cfg::XINSTR], wrel[Cfg::WINSTR];
 #pragma unroll
   for (int j = 0; j < Cfg::XINSTR; ++j) {
-    const int r = (wave * Cfg::XINSTR + j) * RPI + lane / SPR;
-    xoff[j] = (size_t)(m0 + r) * K + stage_swz<BK>(r, lane % SPR) * 8;
+    const int r = (wave * Cfg::XINSTR + j) * 8 + lane / 8;
+    xrel[j] = (size_t)r * K + stage_swz(r, lane % 8) * 8;
   }
 #pragma unroll
   for (int j = 0; j < Cfg::WINSTR; ++j) {
-    const int r = (wave * Cfg::WINSTR + j) * RPI + lane / SPR;
-    woff[j] = (size_t)(n0 + r) * K + stage_swz<BK>(r, lane % SPR) * 8;
+    const int r = (wave * Cfg::WINSTR + j) * 8 + lane / 8;
+    wrel[j] = (size_t)r * K + stage_swz(r, lane % 8) * 8;
   }
-  auto stage = [&](int kt, int slot) {
-    char* xs = smem + slot * Cfg::STAGE + wave * Cfg::XINSTR * 1024;
-    char* ws = smem + slot * Cfg::STAGE + Cfg::XBYTES + wave * Cfg::WINSTR * 1024;
-    const bf16* xk = p.X + kt * BK;
-    const bf16* wk = p.W + kt * BK;
+  auto stage = [&](int ti, int kt, int slot) {
+    int m0, n0;
+    tile_of(ti, m0, n0);
+    const char* xs = smem + slot * Cfg::STAGE + wave * Cfg::XINSTR * 1024;
+    const char* ws = smem + slot * Cfg::STAGE + Cfg::XBYTES + wave * Cfg::WINSTR * 1024;
+    const bf16* xk = p.X + (size_t)m0 * K + kt * BK;
+    const bf16* wk = p.W + (size_t)n0 * K + kt * BK;
 #pragma unroll
-    for (int j = 0; j < Cfg::XINSTR; ++j) glds16_asm(xk + xoff[j], lds_addr(xs + j * 1024));
+    for (int j = 0; j < Cfg::XINSTR; ++j) glds16_asm(xk + xrel[j], lds_addr(xs + j * 1024));
 #pragma unroll
-    for (int j = 0; j < Cfg::WINSTR; ++j) glds16_asm(wk + woff[j], lds_addr(ws + j * 1024));
+    for (int j = 0; j < Cfg::WINSTR; ++j) glds16_asm(wk + wrel[j], lds_addr(ws + j * 1024));
   };
 
   // ---- fragment read offsets --------------------------------------------------------
   // 16x16x32 operand: lane holds row (lane&15), k = 8*(lane>>4) .. +7 of a 32-deep half;
-  // the fragment's rows start at multiples of 16, so the swizzle depends on the lane only.
-  int koff[BK / 32];
+  // fragment rows start at multiples of 16, so the swizzle depends on the lane only.
+  int koff[2];
 #pragma unroll
-  for (int kk = 0; kk < BK / 32; ++kk)
-    koff[kk] = (lane & 15) * ROWB + (stage_swz<BK>(lane & 15, (lane >> 4) + 4 * kk) << 4);
-
-  f32x4 acc[SN][SM];
-#pragma unroll
-  for (int i = 0; i < SN; ++i)
-#pragma unroll
-    for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
+  for (int kk = 0; kk < 2; ++kk)
+    koff[kk] = (lane & 15) * ROWB + (stage_swz(lane & 15, (lane >> 4) + 4 * kk) << 4);
   auto frags = [&](int slot, int kk, bf16x8 (&A)[SN], bf16x8 (&B)[SM]) {
     const char* xs = smem + slot * Cfg::STAGE;
     const char* ws = xs + Cfg::XBYTES;
@@ -128,148 +127,179 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
     for (int j = 0; j < SM; ++j) B[j] = *(const bf16x8*)(xs + (wm * TM + j * 16) * ROWB + koff[kk]);
   };
-  mfma_pipeline<Cfg::S, Cfg::FP, BK / 32, Cfg::XINSTR + Cfg::WINSTR>(K / BK, acc, stage, frags);
 
-  // ---- epilogue ------------------------------------------------------------------
+  f32x4 acc[SN][SM];
+#pragma unroll
+  for (int i = 0; i < SN; ++i)
+#pragma unroll
+    for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- epilogue (per tile) ------------------------------------------------------------
   // acc[i][j][r] = out[m][n] with m = m0 + wm*TM + j*16 + (lane&15),
   //                              n = n0 + wn*TN + i*16 + 4*(lane>>4) + r.
-  const int nq = n0 + wn * TN + 4 * (lane >> 4);
-  const int mrow0 = m0 + wm * TM + (lane & 15);
-  float* red = (float*)smem;  // reuse LDS (all waves passed the final barrier)
+  auto epilogue = [&](int ti, char* scratch) {
+    int m0, n0;
+    tile_of(ti, m0, n0);
+    const int tm = m0 / BM, tn = n0 / BN;
+    const int nq = n0 + wn * TN + 4 * (lane >> 4);
+    const int mrow0 = m0 + wm * TM + (lane & 15);
+    float* red = (float*)scratch;
 
-  if constexpr (MODE == NT_FWD) {
-    const float xs = p.omega * kInv2Pi;
-    float4 bias[SN], hw[SN];
-#pragma unroll
-    for (int i = 0; i < SN; ++i) {
-      const float4 b = *(const float4*)(p.bias + nq + i * 16);
-      bias[i] = float4{b.x * xs, b.y * xs, b.z * xs, b.w * xs};
-      if constexpr (HEAD) hw[i] = *(const float4*)(p.head_w + nq + i * 16);
-    }
-    float hp[SM];
-#pragma unroll
-    for (int j = 0; j < SM; ++j) hp[j] = 0.f;
-#pragma unroll
-    for (int j = 0; j < SM; ++j) {
-      const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
+    if constexpr (MODE == NT_FWD) {
+      const float xs = p.omega * kInv2Pi;
+      float4 bias[SN], hw[SN];
 #pragma unroll
       for (int i = 0; i < SN; ++i) {
-        const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
-        float s[4], c[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
-          // hardware sin/cos inside their reduced domain for any magnitude.
-          const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
-          s[r] = __builtin_amdgcn_sinf(x);
-          c[r] = __builtin_amdgcn_cosf(x);
-        }
-        *(bf16x4*)(p.Y + rowoff + nq + i * 16) = pack4(s[0], s[1], s[2], s[3]);
-        *(bf16x4*)(p.C + rowoff + nq + i * 16) = pack4(c[0], c[1], c[2], c[3]);
-        if constexpr (HEAD)
-          hp[j] += s[0] * hw[i].x + s[1] * hw[i].y + s[2] * hw[i].z + s[3] * hw[i].w;
+        const float4 b = *(const float4*)(p.bias + nq + i * 16);
+        bias[i] = float4{b.x * xs, b.y * xs, b.z * xs, b.w * xs};
+        if constexpr (HEAD) hw[i] = *(const float4*)(p.head_w + nq + i * 16);
       }
-    }
-    if constexpr (HEAD) {
-      // lanes l, l^16, l^32, l^48 hold the same row: fold them, then the WN column waves.
+      float hp[SM];
+#pragma unroll
+      for (int j = 0; j < SM; ++j) hp[j] = 0.f;
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
-        hp[j] += __shfl_xor(hp[j], 16, 64);
-        hp[j] += __shfl_xor(hp[j], 32, 64);
-      }
-      if (lane < 16) {
+        const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
 #pragma unroll
-        for (int j = 0; j < SM; ++j) red[wn * BM + wm * TM + j * 16 + lane] = hp[j];
-      }
-      __syncthreads();
-      if (tid < BM) {
-        float s = 0.f;
+        for (int i = 0; i < SN; ++i) {
+          const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
+          float s[4], c[4];
 #pragma unroll
-        for (int w = 0; w < WN; ++w) s += red[w * BM + tid];
-        p.head_part[(size_t)tn * p.M + m0 + tid] = s;
-      }
-    }
-  } else {
-    // column sums over this block's BM rows (db / dW0 partials): per lane over its SM row
-    // tiles, then through LDS over the 16 row-lanes x WM waves.
-    constexpr int NRED_ROWS = Cfg::WM * 16;
-    const int in_dim = (MODE == NT_DX0) ? p.in_dim : 0;
-    const int nred = 1 + in_dim;
-    float cs[3][SN][4];
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-      for (int i = 0; i < SN; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cs[q][i][r] = 0.f;
-
-    const float om = p.omega;
-#pragma unroll
-    for (int j = 0; j < SM; ++j) {
-      const int m = mrow0 + j * 16;
-      const size_t rowoff = (size_t)m * N;
-      float t0 = 0.f, t1 = 0.f;
-      if constexpr (MODE == NT_DX0) {
-        t0 = p.t[(size_t)m * in_dim];
-        t1 = (in_dim > 1) ? p.t[(size_t)m * in_dim + 1] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < SN; ++i) {
-        const bf16x4 cp = *(const bf16x4*)(p.Cprev + rowoff + nq + i * 16);
-        float dz[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
-          cs[0][i][r] += dz[r];
-          if constexpr (MODE == NT_DX0) {
-            cs[1][i][r] += dz[r] * t0;
-            cs[2][i][r] += dz[r] * t1;
+          for (int r = 0; r < 4; ++r) {
+            // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
+            // hardware sin/cos inside their reduced domain for any magnitude.
+            const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
+            s[r] = __builtin_amdgcn_sinf(x);
+            c[r] = __builtin_amdgcn_cosf(x);
           }
+          *(bf16x4*)(p.Y + rowoff + nq + i * 16) = pack4(s[0], s[1], s[2], s[3]);
+          *(bf16x4*)(p.C + rowoff + nq + i * 16) = pack4(c[0], c[1], c[2], c[3]);
+          if constexpr (HEAD)
+            hp[j] += s[0] * hw[i].x + s[1] * hw[i].y + s[2] * hw[i].z + s[3] * hw[i].w;
         }
-        if constexpr (MODE == NT_DX)
-          *(bf16x4*)(p.dZ + rowoff + nq + i * 16) = pack4(dz[0], dz[1], dz[2], dz[3]);
       }
-    }
-    // partial layout: NT_DX [tm][N]; NT_DX0 [tm][1+in][N] with q=0 -> db0, q=1+j -> dW0[:, j]
+      if constexpr (HEAD) {
+        // lanes l, l^16, l^32, l^48 hold the same row: fold them, then the WN column waves.
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      if (q >= nred) break;
+        for (int j = 0; j < SM; ++j) {
+          hp[j] += __shfl_xor(hp[j], 16, 64);
+          hp[j] += __shfl_xor(hp[j], 32, 64);
+        }
+        lds_barrier();  // every wave is done reading the ring slot used as scratch
+        if (lane < 16) {
 #pragma unroll
-      for (int i = 0; i < SN; ++i)
-        *(float4*)(red + (wm * 16 + (lane & 15)) * RS + wn * TN + i * 16 + 4 * (lane >> 4)) =
-            float4{cs[q][i][0], cs[q][i][1], cs[q][i][2], cs[q][i][3]};
-      __syncthreads();
-      if (tid < BN) {
-        float s = 0.f;
+          for (int j = 0; j < SM; ++j) red[wn * BM + wm * TM + j * 16 + lane] = hp[j];
+        }
+        lds_barrier();
+        if (tid < BM) {
+          float s = 0.f;
+#pragma unroll
+          for (int w = 0; w < WN; ++w) s += red[w * BM + tid];
+          p.head_part[(size_t)tn * p.M + m0 + tid] = s;
+        }
+      }
+    } else {
+      // column sums over this tile's BM rows (db / dW0 partials): per lane over its SM row
+      // tiles, then through LDS over the 16 row-lanes x WM waves.
+      constexpr int NRED_ROWS = Cfg::WM * 16;
+      const int in_dim = (MODE == NT_DX0) ? p.in_dim : 0;
+      const int nred = 1 + in_dim;
+      float cs[3][SN][4];
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int i = 0; i < SN; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cs[q][i][r] = 0.f;
+
+      const float om = p.omega;
+#pragma unroll
+      for (int j = 0; j < SM; ++j) {
+        const int m = mrow0 + j * 16;
+        const size_t rowoff = (size_t)m * N;
+        float t0 = 0.f, t1 = 0.f;
+        if constexpr (MODE == NT_DX0) {
+          t0 = p.t[(size_t)m * in_dim];
+          t1 = (in_dim > 1) ? p.t[(size_t)m * in_dim + 1] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < SN; ++i) {
+          const bf16x4 cp = *(const bf16x4*)(p.Cprev + rowoff + nq + i * 16);
+          float dz[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
+            cs[0][i][r] += dz[r];
+            if constexpr (MODE == NT_DX0) {
+              cs[1][i][r] += dz[r] * t0;
+              cs[2][i][r] += dz[r] * t1;
+            }
+          }
+          if constexpr (MODE == NT_DX)
+            *(bf16x4*)(p.dZ + rowoff + nq + i * 16) = pack4(dz[0], dz[1], dz[2], dz[3]);
+        }
+      }
+      // partial layout: NT_DX [tm][N]; NT_DX0 [tm][1+in][N] with q=0 -> db0, q=1+j -> dW0[:, j]
+      lds_barrier();  // every wave is done reading the ring slot used as scratch
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        if (q >= nred) break;
+#pragma unroll
+        for (int i = 0; i < SN; ++i)
+          *(float4*)(red + (wm * 16 + (lane & 15)) * RS + wn * TN + i * 16 + 4 * (lane >> 4)) =
+              float4{cs[q][i][0], cs[q][i][1], cs[q][i][2], cs[q][i][3]};
+        lds_barrier();
+        if (tid < BN) {
+          float s = 0.f;
 #pragma unroll 8
-        for (int r = 0; r < NRED_ROWS; ++r) s += red[r * RS + tid];
-        p.colsum_part[((size_t)tm * nred + q) * N + n0 + tid] = s;
+          for (int r = 0; r < NRED_ROWS; ++r) s += red[r * RS + tid];
+          p.colsum_part[((size_t)tm * nred + q) * N + n0 + tid] = s;
+        }
+        lds_barrier();
       }
-      __syncthreads();
     }
-  }
+  };
+
+  mfma_pipeline_tiles<2, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
+      my_tiles, K / BK, acc, smem, Cfg::STAGE, stage, frags, epilogue);
 }
 
+static int g_num_cus = 0;
+static int g_nt_grid_cap = 0;  // test hook: persistent grid size (0 = one block per CU)
+void gemm_nt_set_grid_cap(int cap) { g_nt_grid_cap = cap; }
+
 template <class Cfg, int MODE, bool HEAD>
-static hipError_t launch_nt(const NtParams& p, hipStream_t s) {
-  const int grid = (p.M / Cfg::BM) * (p.N / Cfg::BN);
+static hipError_t launch_nt(const NtParams& p, hipStream_t s, bool persistent) {
+  const int ntiles = (p.M / Cfg::BM) * (p.N / Cfg::BN);
+  if (g_num_cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        g_num_cus <= 0)
+      g_num_cus = 256;
+  }
+  const int cap = g_nt_grid_cap > 0 ? g_nt_grid_cap : g_num_cus;
+  const int grid = persistent ? (ntiles < cap ? ntiles : cap) : ntiles;
   hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD>), dim3(grid), dim3(Cfg::THREADS), 0, s, p);
   return hipGetLastError();
 }
 
 template <class Cfg>
-static hipError_t dispatch_mode(int mode, bool head, const NtParams& p, hipStream_t s) {
+static hipError_t dispatch_mode(int mode, bool head, const NtParams& p, hipStream_t s, bool persistent) {
   switch (mode) {
-    case NT_FWD: return head ? launch_nt<Cfg, NT_FWD, true>(p, s) : launch_nt<Cfg, NT_FWD, false>(p, s);
-    case NT_DX: return launch_nt<Cfg, NT_DX, false>(p, s);
-    case NT_DX0: return launch_nt<Cfg, NT_DX0, false>(p, s);
+    case NT_FWD:
+      return head ? launch_nt<Cfg, NT_FWD, true>(p, s, persistent)
+                  : launch_nt<Cfg, NT_FWD, false>(p, s, persistent);
+    case NT_DX: return launch_nt<Cfg, NT_DX, false>(p, s, persistent);
+    case NT_DX0: return launch_nt<Cfg, NT_DX0, false>(p, s, persistent);
   }
   return hipErrorInvalidValue;
 }
 
-// tile override for A/B measurement: 0 = auto, 128 or 256
+// tile override for A/B measurement: 0 = auto, 128 or 256; pipe: 1 = persistent 256x256
+// (default), 0 = one tile per block
 static int g_nt_tile = 0;
-static int g_nt_pipe = 1;  // default 256x256 pipeline variant (see NtL*)
+static int g_nt_pipe = 1;
 void gemm_nt_set_tile(int tile) { g_nt_tile = tile; }
 void gemm_nt_set_pipe(int v) { g_nt_pipe = v; }
 
@@ -277,7 +307,7 @@ int nt_choose_tile(int M, int N) {
   const bool large_ok = (M % 256 == 0) && (N % 256 == 0);
   if (g_nt_tile == 128 || !large_ok) return 128;
   if (g_nt_tile == 256) return 256;
-  // the 256x256 tile (1 block/CU) needs >= 2 blocks per CU to keep 256 CUs busy
+  // the 256x256 tile (1 block/CU) needs >= 2 tiles per CU to keep 256 CUs busy
   return (long)(M / 256) * (N / 256) >= 512 ? 256 : 128;
 }
 
@@ -286,15 +316,10 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (mode == NT_DX0 && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
   if (p.tile == 256) {
     if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
-    switch (g_nt_pipe) {
-      case 0: return dispatch_mode<NtL0>(mode, head, p, s);
-      case 1: return dispatch_mode<NtL1>(mode, head, p, s);
-      case 2: return dispatch_mode<NtL2>(mode, head, p, s);
-    }
-    return hipErrorInvalidValue;
+    return dispatch_mode<NtLarge>(mode, head, p, s, g_nt_pipe != 0);
   }
   if (p.tile != 128) return hipErrorInvalidValue;
-  return dispatch_mode<NtSmall>(mode, head, p, s);
+  return dispatch_mode<NtSmall>(mode, head, p, s, false);
 }
 
 }  // namespace siren

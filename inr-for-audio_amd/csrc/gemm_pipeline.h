@@ -110,4 +110,73 @@ __device__ __forceinline__ void mfma_pipeline(int nk, f32x4 (&acc)[NA][NB], Stag
   __builtin_amdgcn_s_barrier();
 }
 
+// Persistent variant for short-K GEMMs (K = hidden width, 16 K-steps per tile): the block
+// walks `ntiles` tiles and the double-buffered ring runs straight across tile boundaries, so
+// the first stage of tile i+1 is in flight while tile i's epilogue runs, and the epilogue's
+// global stores drain under tile i+1's first K-step.
+//   stage(tile, kt, slot)  issues the LDS-DMA of K-step kt of the block's tile-th tile;
+//   frags(slot, kk, A, B)  reads one k32 half of the operand fragments;
+//   epi(tile, scratch)     consumes acc; `scratch` is the ring slot just read (free until the
+//                          next step's barrier; an epilogue that uses it must first
+//                          s_waitcnt lgkmcnt(0) + s_barrier, and may only use raw barriers).
+// SLACK = vector-memory instructions (stores) the epilogue issues after the prefetch of the
+// next stage: the first wait after an epilogue is vmcnt(SLACK), which still covers the
+// (older) prefetch because vmcnt retires in issue order.  SLACK must not exceed the real
+// count; 0 is always safe.
+template <int KK, int G, int NA, int NB, int SLACK, class StageFn, class FragFn, class EpiFn>
+__device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&acc)[NA][NB],
+                                                    char* smem, int stage_bytes, StageFn&& stage,
+                                                    FragFn&& frags, EpiFn&& epi) {
+  static_assert(SLACK >= 0 && SLACK < 64, "vmcnt immediate");
+  const int total = ntiles * nk;
+  if (total <= 0) return;
+  int it = 0, ik = 0;  // issue pointer
+  stage(it, ik, 0);
+  if (++ik == nk) { ik = 0; ++it; }
+  int ct = 0, ck = 0, slot = 0;
+  bool after_epi = false;
+  for (int u = 0; u < total; ++u) {
+    if (after_epi) wait_vmcnt<SLACK>();
+    else wait_vmcnt<0>();
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    if (u + 1 < total) {
+      stage(it, ik, slot ^ 1);
+      if (++ik == nk) { ik = 0; ++it; }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8 A[NA], B[NB];
+      frags(slot, kk, A, B);
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    after_epi = false;
+    if (++ck == nk) {
+      epi(ct, smem + slot * stage_bytes);
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ck = 0;
+      ++ct;
+      after_epi = true;
+    }
+    slot ^= 1;
+  }
+  wait_vmcnt<0>();
+  wait_lgkm0();
+  __builtin_amdgcn_s_barrier();
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  wait_lgkm0();
+  __builtin_amdgcn_s_barrier();
+}
+
 }  // namespace siren

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
 }
 
 static int g_tn_tile = 0;
-static int g_tn_pipe = 1;
+static int g_tn_pipe = 0;  // BK 64 double buffer: fastest measured (r01 A/B)
 void gemm_tn_set_tile(int tile) { g_tn_tile = tile; }
 void gemm_tn_set_pipe(int v) { g_tn_pipe = v; }
 

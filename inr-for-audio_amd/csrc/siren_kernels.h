@@ -35,8 +35,9 @@ int nt_choose_tile(int M, int N);
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s);
 void gemm_nt_set_tile(int tile);  // 0 = auto, 128, 256 (A/B measurement)
 void gemm_tn_set_tile(int tile);
-void gemm_nt_set_pipe(int v);     // 256x256 K-loop variant (NtL0..NtL2)
-void gemm_tn_set_pipe(int v);     // (TnL0..TnL2)
+void gemm_nt_set_pipe(int v);     // 1 = persistent 256x256 (default), 0 = one tile per block
+void gemm_tn_set_pipe(int v);     // 256x256 K-loop variant (TnL0..TnL2)
+void gemm_nt_set_grid_cap(int cap);  // persistent grid size override (0 = #CUs)
 
 struct TnParams {
   const bf16* Y;   // [R][Hin]   layer input (A role: dW column index k)

@@ -69,6 +69,7 @@ def test_train_step_forced_tiles(lib, dev, tile):
     bench uses) against the oracle, SIREN 5x512 on 2048 rows."""
     from inr_for_audio_amd.engine import SirenEngine
     assert lib.siren_set_option(0, tile) == 0 and lib.siren_set_option(1, tile) == 0
+    assert lib.siren_set_option(4, 3) == 0   # persistent NT grid of 3 blocks: multi-tile walks
     try:
         L, H, w0 = 4, 512, 3000.0
         model = _model(H, L, w0)
@@ -80,6 +81,7 @@ def test_train_step_forced_tiles(lib, dev, tile):
     finally:
         lib.siren_set_option(0, 0)
         lib.siren_set_option(1, 0)
+        lib.siren_set_option(4, 0)
     got = {k: v.detach().cpu().numpy() for k, v in zip(eng.layout.names, eng.grad_views())}
     p = orc.Params.from_state_dict(sd0, L)
     out, cache = orc.forward(p, t.numpy(), w0, 30.0, bf16=True, dtype=np.float64)

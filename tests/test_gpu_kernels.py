@@ -49,23 +49,26 @@ def _release():
     _KEEP.clear()
 
 
-@pytest.fixture(params=[(128, 0), (256, 0), (256, 1), (256, 2)], ids=lambda p: f"t{p[0]}p{p[1]}")
+@pytest.fixture(params=[(128, 0, 0), (256, 0, 0), (256, 1, 0), (256, 1, 2)],
+                ids=lambda p: f"t{p[0]}p{p[1]}g{p[2]}")
 def nt_tile(request, lib):
-    """Force the NT GEMM tile edge and 256x256 K-loop variant (siren_set_option) for the
-    duration of one test."""
-    tile, pipe = request.param
+    """Force the NT GEMM tile edge, persistence and persistent grid size (siren_set_option)
+    for one test; grid 2 makes every block walk several tiles across the LDS ring."""
+    tile, pipe, grid = request.param
     ok(lib.siren_set_option(0, tile), lib)
     ok(lib.siren_set_option(2, pipe), lib)
+    ok(lib.siren_set_option(4, grid), lib)
     yield tile
     lib.siren_set_option(0, 0)
     lib.siren_set_option(2, 1)
+    lib.siren_set_option(4, 0)
 
 
 @pytest.fixture(params=[0, 1, 2], ids=lambda p: f"p{p}")
 def tn_pipe(request, lib):
     ok(lib.siren_set_option(3, request.param), lib)
     yield request.param
-    lib.siren_set_option(3, 1)
+    lib.siren_set_option(3, 0)
 
 
 def _skip_tile(tile, R, H):
@@ -241,7 +244,7 @@ def test_first_bwd_dx(lib, dev, in_dim, omega0, nt_tile):
                                              (512, 1024, 2, 128), (640, 512, 5, 128), (1024, 256, 3, 256),
                                              (2048, 512, 7, 256), (512, 1024, 2, 256), (320, 256, 9, 256)])
 def test_inner_bwd_dw(lib, dev, R, H, splits, tile, tn_pipe):
-    if tile == 128 and tn_pipe != 1:
+    if tile == 128 and tn_pipe != 0:
         pytest.skip("pipeline variants apply to the 256x256 tile")
     rng = np.random.default_rng(7)
     Y = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))

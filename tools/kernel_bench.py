@@ -98,8 +98,10 @@ def main():
     for _ in range(args.rounds):
         for name, (tile, pipe, fn, _) in cases.items():
             lib.siren_set_option(0, tile if not name.startswith("dw") else 0)
-            lib.siren_set_option(2, pipe)
-            lib.siren_set_option(3, pipe)
+            if name.startswith("dw"):
+                lib.siren_set_option(3, pipe)
+            else:
+                lib.siren_set_option(2, min(pipe, 1))
             for _ in range(1):
                 _lib.check(fn(), name)
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -111,7 +113,7 @@ def main():
             times[name].append(ev0.elapsed_time(ev1) / args.reps)
     lib.siren_set_option(0, 0)
     lib.siren_set_option(2, 1)
-    lib.siren_set_option(3, 1)
+    lib.siren_set_option(3, 0)
     out = {}
     for name, (tile, pipe, fn, fl) in cases.items():
         ts = sorted(times[name])
