@@ -185,10 +185,13 @@ enum siren_prof_kind {
  * SIREN_OPT_TN_PIPE = 0..2 selects the 256x256 dW K-loop (0: BK 64 double buffer
  * (default), 1: BK 32 4-slot ring, 2: BK 32 5-slot ring);
  * SIREN_OPT_NT_GRID = persistent NT grid size (0 = one block per CU; tests use small
- * values so every block walks several tiles). */
+ * values so every block walks several tiles);
+ * SIREN_OPT_NT_STAGGER = persistent NT start stagger: block b idles (b % 16) * value units of
+ * ~1.7k cycles before its first tile, so that the blocks' epilogue store bursts do not
+ * coincide (0 = none; 0..64). */
 enum siren_option {
   SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1, SIREN_OPT_NT_PIPE = 2, SIREN_OPT_TN_PIPE = 3,
-  SIREN_OPT_NT_GRID = 4
+  SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_STAGGER = 5
 };
 int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);

@@ -13,16 +13,20 @@
 //
 // Tiles: 256x256 with 8 waves (2x4, each 128x64 = 8x4 v_mfma_f32_16x16x32_bf16 tiles),
 // PERSISTENT: one block per CU walks its tiles and the double-buffered LDS ring runs across
-// tile boundaries (gemm_pipeline.h mfma_pipeline_tiles), so tile i+1's first operand stage
-// is loading while tile i's epilogue runs and the epilogue's stores drain under tile i+1's
-// MFMAs.  A 128x128 / 4-wave config (2 blocks per CU, one tile per block) serves grids too
-// small for 256x256.  Operands are staged HBM->LDS by LDS-DMA (global_load_lds_dwordx4 from
-// inline asm), with an XOR swizzle on the SOURCE address so that the ds_read_b128 fragment
-// reads are bank-conflict free (cdna_hip_programming.md §5.4 rule 21 / T2).
+// tile boundaries (gemm_pipeline.h mfma_pipeline_tiles): both first operand stages of tile
+// i+1 are in flight before tile i's epilogue issues its stores, which then drain under
+// tile i+1's first two K-steps.  A 128x128 / 4-wave config (2 blocks per CU, one tile per
+// block) serves grids too small for 256x256.  Operands are staged HBM->LDS by LDS-DMA
+// (global_load_lds_dwordx4 from inline asm), with an XOR swizzle on the SOURCE address so
+// that the ds_read_b128 fragment reads are bank-conflict free (cdna_hip_programming.md
+// §5.4 rule 21 / T2).
 //
 // MFMA operand roles are swapped (A := W rows, B := X rows) so each lane ends up holding 4
-// consecutive output COLUMNS of one row: 8-byte contiguous bf16 stores, and per-row bias
-// loads as one float4.
+// consecutive output COLUMNS of one row (per-row bias loads as one float4); adjacent column
+// subtiles are then exchanged across 16-lane groups (swap16_pair) so every epilogue store
+// and Cprev load is a 16-B row piece.  The epilogue's store tail is issue-bound (measured:
+// 64 scattered dwordx2 per lane cost 1.0 ms of a 2.8 ms forward GEMM), so halving the
+// instruction count and keeping the stores behind two prefetched stages is what matters.
 #include "gemm_pipeline.h"
 #include "siren_common.h"
 #include "siren_kernels.h"
@@ -41,28 +45,31 @@ struct NtCfg {
   static constexpr int ROWB = BK * 2;               // bytes per staged row
   static constexpr int XBYTES = BM * ROWB, WBYTES = BN * ROWB;
   static constexpr int STAGE = XBYTES + WBYTES;
-  static constexpr int LDS = 2 * STAGE;
+  static constexpr int RING = 2 * STAGE;
+  // epilogue scratch behind the ring: HEAD row partials [WN][BM] or column sums [3][WM][BN],
+  // then (NT_FWD) the whole bias and head weight vectors, staged once per block
+  static constexpr int RED = 4 * (WN * BM > 3 * WM * BN ? WN * BM : 3 * WM * BN);
+  static constexpr int MAXN = 1024;
+  static constexpr int LDS = RING + RED + 2 * 4 * MAXN;
   static constexpr int XINSTR = XBYTES / 1024 / NWAVES;  // LDS-DMA instructions per wave per stage
   static constexpr int WINSTR = WBYTES / 1024 / NWAVES;
-  static constexpr int RED_STRIDE = BN + 4;
   static_assert(XBYTES % (1024 * NWAVES) == 0 && WBYTES % (1024 * NWAVES) == 0, "staging split");
-  static_assert(WM * 16 * RED_STRIDE * 4 <= STAGE && WN * BM * 4 <= STAGE, "epilogue scratch in one slot");
+  static_assert(SN % 2 == 0, "16-B row pieces pair adjacent column subtiles");
+  static_assert(LDS <= 160 * 1024, "LDS");
 };
 using NtSmall = NtCfg<128, 128, 2, 2>;
 using NtLarge = NtCfg<256, 256, 2, 4>;
 
-// store instructions an epilogue issues per wave (lower bound; see mfma_pipeline_tiles)
+// store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
 constexpr int epilogue_stores() {
-  return MODE == NT_FWD ? (2 * Cfg::SM * Cfg::SN > 63 ? 63 : 2 * Cfg::SM * Cfg::SN)
-                        : (MODE == NT_DX ? Cfg::SM * Cfg::SN : 0);
+  return MODE == NT_FWD ? Cfg::SM * Cfg::SN : (MODE == NT_DX ? Cfg::SM * Cfg::SN / 2 : 0);
 }
 
 template <class Cfg, int MODE, bool HEAD>
 __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, BK = Cfg::BK, WN = Cfg::WN;
   constexpr int TM = Cfg::TM, TN = Cfg::TN, SM = Cfg::SM, SN = Cfg::SN;
-  constexpr int RS = Cfg::RED_STRIDE;
   __shared__ __attribute__((aligned(16))) char smem[Cfg::LDS];
 
   const int tid = threadIdx.x;
@@ -77,6 +84,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   const int G = gridDim.x;
   const int bp = xcd_remap(blockIdx.x, G);
   const int my_tiles = (ntiles - bp + G - 1) / G;
+  // Start stagger: blocks that run in lockstep hit their epilogues together and their
+  // stores then arrive as one chip-wide burst; spreading the starts over a tile's duration
+  // spreads the bursts.
+  for (int i = (bp & 15) * p.stagger; i > 0; --i) __builtin_amdgcn_s_sleep(27);
   auto tile_of = [&](int i, int& m0, int& n0) {
     const int g = bp + i * G;
     const int tm = g / tiles_n;
@@ -137,22 +148,61 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // ---- epilogue (per tile) ------------------------------------------------------------
   // acc[i][j][r] = out[m][n] with m = m0 + wm*TM + j*16 + (lane&15),
   //                              n = n0 + wn*TN + i*16 + 4*(lane>>4) + r.
-  auto epilogue = [&](int ti, char* scratch) {
+  // Global traffic goes in 16-B row pieces: column subtiles (2p, 2p+1) are exchanged with
+  // swap16_pair, this lane's piece starting at column ncol + 32p + swap16_col(lane).
+  float* red = (float*)(smem + Cfg::RING);
+  // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
+  // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
+  float* bias_lds = (float*)(smem + Cfg::RING + Cfg::RED);
+  float* hw_lds = bias_lds + Cfg::MAXN;
+  if constexpr (MODE == NT_FWD) {
+    for (int c = tid * 4; c < N; c += Cfg::THREADS * 4) {
+      *(float4*)(bias_lds + c) = *(const float4*)(p.bias + c);
+      if constexpr (HEAD) *(float4*)(hw_lds + c) = *(const float4*)(p.head_w + c);
+    }
+    // visible to other waves after the pipeline's first barrier
+  }
+  // NT_DX / NT_DX0 epilogue operands loaded by `pre` (before the next tile's early prefetch)
+  constexpr int PRE_J = (MODE == NT_FWD) ? 0 : (MODE == NT_DX ? SM : SM / 2);
+  uint4 cp_in[PRE_J > 0 ? PRE_J : 1][SN / 2];
+  float t_in[SM][2];
+  auto pre = [&](int ti) {
+    int m0, n0;
+    tile_of(ti, m0, n0);
+    const int npc = n0 + wn * TN + swap16_col(lane);
+    const int mrow0 = m0 + wm * TM + (lane & 15);
+    if constexpr (MODE != NT_FWD) {
+#pragma unroll
+      for (int j = 0; j < PRE_J; ++j)
+#pragma unroll
+        for (int pp = 0; pp < SN / 2; ++pp)
+          cp_in[j][pp] = *(const uint4*)(p.Cprev + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
+      if constexpr (MODE == NT_DX0) {
+#pragma unroll
+        for (int j = 0; j < SM; ++j) {
+          const size_t m = mrow0 + j * 16;
+          t_in[j][0] = p.t[m * p.in_dim];
+          t_in[j][1] = (p.in_dim > 1) ? p.t[m * p.in_dim + 1] : 0.f;
+        }
+      }
+    }
+  };
+  auto epilogue = [&](int ti) {
     int m0, n0;
     tile_of(ti, m0, n0);
     const int tm = m0 / BM, tn = n0 / BN;
-    const int nq = n0 + wn * TN + 4 * (lane >> 4);
+    const int npc = n0 + wn * TN + swap16_col(lane);      // swapped layout: this lane's piece
     const int mrow0 = m0 + wm * TM + (lane & 15);
-    float* red = (float*)scratch;
 
     if constexpr (MODE == NT_FWD) {
+      const int nq = n0 + wn * TN + 4 * (lane >> 4);     // natural layout: this lane's columns
       const float xs = p.omega * kInv2Pi;
       float4 bias[SN], hw[SN];
 #pragma unroll
       for (int i = 0; i < SN; ++i) {
-        const float4 b = *(const float4*)(p.bias + nq + i * 16);
+        const float4 b = *(const float4*)(bias_lds + nq + i * 16);
         bias[i] = float4{b.x * xs, b.y * xs, b.z * xs, b.w * xs};
-        if constexpr (HEAD) hw[i] = *(const float4*)(p.head_w + nq + i * 16);
+        if constexpr (HEAD) hw[i] = *(const float4*)(hw_lds + nq + i * 16);
       }
       float hp[SM];
 #pragma unroll
@@ -161,21 +211,28 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       for (int j = 0; j < SM; ++j) {
         const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
 #pragma unroll
-        for (int i = 0; i < SN; ++i) {
-          const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
-          float s[4], c[4];
+        for (int pp = 0; pp < SN / 2; ++pp) {
+          uint2 ys[2], cs[2];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
-            // hardware sin/cos inside their reduced domain for any magnitude.
-            const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
-            s[r] = __builtin_amdgcn_sinf(x);
-            c[r] = __builtin_amdgcn_cosf(x);
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * pp + h;
+            const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
+            float s[4], c[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
+              // hardware sin/cos inside their reduced domain for any magnitude.
+              const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
+              s[r] = __builtin_amdgcn_sinf(x);
+              c[r] = __builtin_amdgcn_cosf(x);
+            }
+            ys[h] = as_u2(pack4(s[0], s[1], s[2], s[3]));
+            cs[h] = as_u2(pack4(c[0], c[1], c[2], c[3]));
+            if constexpr (HEAD)
+              hp[j] += s[0] * hw[i].x + s[1] * hw[i].y + s[2] * hw[i].z + s[3] * hw[i].w;
           }
-          *(bf16x4*)(p.Y + rowoff + nq + i * 16) = pack4(s[0], s[1], s[2], s[3]);
-          *(bf16x4*)(p.C + rowoff + nq + i * 16) = pack4(c[0], c[1], c[2], c[3]);
-          if constexpr (HEAD)
-            hp[j] += s[0] * hw[i].x + s[1] * hw[i].y + s[2] * hw[i].z + s[3] * hw[i].w;
+          *(uint4*)(p.Y + rowoff + npc + pp * 32) = swap16_pair(ys[0], ys[1]);
+          *(uint4*)(p.C + rowoff + npc + pp * 32) = swap16_pair(cs[0], cs[1]);
         }
       }
       if constexpr (HEAD) {
@@ -185,7 +242,6 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           hp[j] += __shfl_xor(hp[j], 16, 64);
           hp[j] += __shfl_xor(hp[j], 32, 64);
         }
-        lds_barrier();  // every wave is done reading the ring slot used as scratch
         if (lane < 16) {
 #pragma unroll
           for (int j = 0; j < SM; ++j) red[wn * BM + wm * TM + j * 16 + lane] = hp[j];
@@ -200,8 +256,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       }
     } else {
       // column sums over this tile's BM rows (db / dW0 partials): per lane over its SM row
-      // tiles, then through LDS over the 16 row-lanes x WM waves.
-      constexpr int NRED_ROWS = Cfg::WM * 16;
+      // tiles, over the 16 row-lanes by DPP, then over the WM row waves through LDS.
       const int in_dim = (MODE == NT_DX0) ? p.in_dim : 0;
       const int nred = 1 + in_dim;
       float cs[3][SN][4];
@@ -219,57 +274,82 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         const size_t rowoff = (size_t)m * N;
         float t0 = 0.f, t1 = 0.f;
         if constexpr (MODE == NT_DX0) {
-          t0 = p.t[(size_t)m * in_dim];
-          t1 = (in_dim > 1) ? p.t[(size_t)m * in_dim + 1] : 0.f;
+          t0 = t_in[j][0];
+          t1 = t_in[j][1];
         }
 #pragma unroll
-        for (int i = 0; i < SN; ++i) {
-          const bf16x4 cp = *(const bf16x4*)(p.Cprev + rowoff + nq + i * 16);
-          float dz[4];
+        for (int pp = 0; pp < SN / 2; ++pp) {
+          uint2 cpu[2];
+          const uint4 cpv = (j < PRE_J) ? cp_in[j < PRE_J ? j : 0][pp]
+                                        : *(const uint4*)(p.Cprev + rowoff + npc + pp * 32);
+          unswap16_pair(cpv, cpu[0], cpu[1]);
+          uint2 dzp[2];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
-            cs[0][i][r] += dz[r];
-            if constexpr (MODE == NT_DX0) {
-              cs[1][i][r] += dz[r] * t0;
-              cs[2][i][r] += dz[r] * t1;
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * pp + h;
+            const bf16x4 cp = as_bf4(cpu[h]);
+            float dz[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
+              cs[0][i][r] += dz[r];
+              if constexpr (MODE == NT_DX0) {
+                cs[1][i][r] += dz[r] * t0;
+                cs[2][i][r] += dz[r] * t1;
+              }
             }
+            dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
           }
           if constexpr (MODE == NT_DX)
-            *(bf16x4*)(p.dZ + rowoff + nq + i * 16) = pack4(dz[0], dz[1], dz[2], dz[3]);
+            *(uint4*)(p.dZ + rowoff + npc + pp * 32) = swap16_pair(dzp[0], dzp[1]);
         }
       }
       // partial layout: NT_DX [tm][N]; NT_DX0 [tm][1+in][N] with q=0 -> db0, q=1+j -> dW0[:, j]
-      lds_barrier();  // every wave is done reading the ring slot used as scratch
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         if (q >= nred) break;
 #pragma unroll
-        for (int i = 0; i < SN; ++i)
-          *(float4*)(red + (wm * 16 + (lane & 15)) * RS + wn * TN + i * 16 + 4 * (lane >> 4)) =
-              float4{cs[q][i][0], cs[q][i][1], cs[q][i][2], cs[q][i][3]};
-        lds_barrier();
-        if (tid < BN) {
+        for (int i = 0; i < SN; ++i) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[q][i][r]);
+          if ((lane & 15) == 0)
+            *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + i * 16 + 4 * (lane >> 4)) =
+                float4{v[0], v[1], v[2], v[3]};
+        }
+      }
+      lds_barrier();
+      if (tid < BN) {
+        for (int q = 0; q < nred; ++q) {
           float s = 0.f;
-#pragma unroll 8
-          for (int r = 0; r < NRED_ROWS; ++r) s += red[r * RS + tid];
+#pragma unroll
+          for (int w = 0; w < Cfg::WM; ++w) s += red[(q * Cfg::WM + w) * BN + tid];
           p.colsum_part[((size_t)tm * nred + q) * N + n0 + tid] = s;
         }
-        lds_barrier();
       }
     }
   };
 
   mfma_pipeline_tiles<2, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
-      my_tiles, K / BK, acc, smem, Cfg::STAGE, stage, frags, epilogue);
+      my_tiles, K / BK, acc, stage, frags, pre, epilogue, p.stamps);
 }
 
 static int g_num_cus = 0;
 static int g_nt_grid_cap = 0;  // test hook: persistent grid size (0 = one block per CU)
 void gemm_nt_set_grid_cap(int cap) { g_nt_grid_cap = cap; }
+static int g_nt_stagger = 0;
+void gemm_nt_set_stagger(int units) { g_nt_stagger = units; }
+static unsigned long long* g_nt_stamps = nullptr;
+#ifdef SIREN_NT_STAMPS
+// diagnostic builds only: [grid][256 tiles][4] u64 device buffer, or null to stop recording
+extern "C" void siren_debug_nt_stamps(void* buf) { g_nt_stamps = (unsigned long long*)buf; }
+#endif
 
 template <class Cfg, int MODE, bool HEAD>
-static hipError_t launch_nt(const NtParams& p, hipStream_t s, bool persistent) {
+static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent) {
+  NtParams p = p_in;
+  p.stagger = persistent ? g_nt_stagger : 0;
+  p.stamps = g_nt_stamps;
   const int ntiles = (p.M / Cfg::BM) * (p.N / Cfg::BN);
   if (g_num_cus == 0) {
     int dev = 0;
@@ -312,7 +392,7 @@ int nt_choose_tile(int M, int N) {
 }
 
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
-  if (p.M % NtSmall::BM || p.N % NtSmall::BN || p.K % NtSmall::BK || p.M <= 0) return hipErrorInvalidValue;
+  if (p.M % NtSmall::BM || p.N % NtSmall::BN || p.K % NtSmall::BK || p.M <= 0 || p.N > NtSmall::MAXN) return hipErrorInvalidValue;
   if (mode == NT_DX0 && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
   if (p.tile == 256) {
     if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;

@@ -110,40 +110,75 @@ __device__ __forceinline__ void mfma_pipeline(int nk, f32x4 (&acc)[NA][NB], Stag
   __builtin_amdgcn_s_barrier();
 }
 
+__device__ __forceinline__ void lds_barrier() {
+  wait_lgkm0();
+  __builtin_amdgcn_s_barrier();
+}
+
 // Persistent variant for short-K GEMMs (K = hidden width, 16 K-steps per tile): the block
-// walks `ntiles` tiles and the double-buffered ring runs straight across tile boundaries, so
-// the first stage of tile i+1 is in flight while tile i's epilogue runs, and the epilogue's
-// global stores drain under tile i+1's first K-step.
+// walks `ntiles` tiles and the double-buffered ring runs straight across tile boundaries.
+// vmcnt retires loads AND stores in issue order (MI355X_MICROARCH.md §vmcnt), so a stage
+// issued after an epilogue's stores cannot be waited for without waiting for the stores too.
+// Hence at a tile boundary BOTH first stages of the next tile are issued before the
+// epilogue runs: stage k0 at the top of the last K-step as usual, stage k1 into the slot the
+// last K-step just read (one extra barrier per tile).  The next tile's K-steps 0 and 1 then
+// wait with vmcnt(G + SLACK) and vmcnt(SLACK) -- the stores keep draining under two K-steps
+// of MFMAs -- and only K-step 2 waits for them.
 //   stage(tile, kt, slot)  issues the LDS-DMA of K-step kt of the block's tile-th tile;
 //   frags(slot, kk, A, B)  reads one k32 half of the operand fragments;
-//   epi(tile, scratch)     consumes acc; `scratch` is the ring slot just read (free until the
-//                          next step's barrier; an epilogue that uses it must first
-//                          s_waitcnt lgkmcnt(0) + s_barrier, and may only use raw barriers).
-// SLACK = vector-memory instructions (stores) the epilogue issues after the prefetch of the
-// next stage: the first wait after an epilogue is vmcnt(SLACK), which still covers the
-// (older) prefetch because vmcnt retires in issue order.  SLACK must not exceed the real
-// count; 0 is always safe.
-template <int KK, int G, int NA, int NB, int SLACK, class StageFn, class FragFn, class EpiFn>
+//   pre(tile)              issues the epilogue's own global loads (bias, Cprev, ...) BEFORE
+//                          the early prefetch, so that waiting for them does not wait for it;
+//   epi(tile)              consumes acc; the ring is NOT available to it (own LDS scratch;
+//                          raw barriers only -- every wave calls epi the same number of times).
+// SLACK = vector-memory instructions every wave's epilogue issues (a lower bound; 0 is always
+// safe).  G = LDS-DMA instructions per wave per stage.
+// SIREN_NT_STAMPS (diagnostic builds only, tools/nt_stamps.py): thread 0 of each block
+// records per tile {start, cycles in K-step waits+barriers, end of MFMAs, end of epilogue}
+// with s_memtime into stamps[block][tile][4].
+#ifdef SIREN_NT_STAMPS
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#endif
+
+template <int KK, int G, int NA, int NB, int SLACK, class StageFn, class FragFn, class PreFn,
+          class EpiFn>
 __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&acc)[NA][NB],
-                                                    char* smem, int stage_bytes, StageFn&& stage,
-                                                    FragFn&& frags, EpiFn&& epi) {
-  static_assert(SLACK >= 0 && SLACK < 64, "vmcnt immediate");
+                                                    StageFn&& stage, FragFn&& frags, PreFn&& pre,
+                                                    EpiFn&& epi,
+                                                    unsigned long long* stamps = nullptr) {
+  static_assert(SLACK >= 0 && G + SLACK < 64, "vmcnt immediate");
   const int total = ntiles * nk;
   if (total <= 0) return;
-  int it = 0, ik = 0;  // issue pointer
-  stage(it, ik, 0);
-  if (++ik == nk) { ik = 0; ++it; }
+#ifdef SIREN_NT_STAMPS
+  unsigned long long st_tile = 0, st_wait = 0, st_a = 0;
+  stamps = stamps ? stamps + (size_t)blockIdx.x * 256 * 4 : nullptr;
+  const bool st_on = stamps && threadIdx.x == 0;
+#define SIREN_STAMP(x) x
+#else
+#define SIREN_STAMP(x)
+#endif
+  int it = 0, ik = 0;  // issue pointer (tile, K-step)
+  int issued = 0;      // stages issued so far (global step index of the next one)
+  auto issue = [&](int slot) {
+    stage(it, ik, slot);
+    if (++ik == nk) { ik = 0; ++it; }
+    ++issued;
+  };
+  issue(0);
   int ct = 0, ck = 0, slot = 0;
-  bool after_epi = false;
+  int after = 0;  // 1: first K-step after an epilogue with the early prefetch, 2: second
   for (int u = 0; u < total; ++u) {
-    if (after_epi) wait_vmcnt<SLACK>();
+    SIREN_STAMP(st_a = stamp_now(); if (ck == 0) { st_tile = st_a; st_wait = 0; })
+    if (after == 1) wait_vmcnt<G + SLACK>();
+    else if (after == 2) wait_vmcnt<SLACK>();
     else wait_vmcnt<0>();
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
-    if (u + 1 < total) {
-      stage(it, ik, slot ^ 1);
-      if (++ik == nk) { ik = 0; ++it; }
-    }
+    SIREN_STAMP(st_wait += stamp_now() - st_a;)
+    if (issued == u + 1 && issued < total) issue(slot ^ 1);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
@@ -156,27 +191,38 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
-    after_epi = false;
+    after = (after == 1) ? 2 : 0;
     if (++ck == nk) {
-      epi(ct, smem + slot * stage_bytes);
+      SIREN_STAMP(const unsigned long long st_c = stamp_now();)
+      pre(ct);
+      if (issued == u + 2 && issued < total) {
+        lds_barrier();  // every wave is done reading `slot`
+        issue(slot);
+        after = 1;
+      } else {
+        after = 2;      // only the (older) next stage is outstanding besides the stores
+      }
+      epi(ct);
+      SIREN_STAMP(if (st_on && ct < 256) {
+        const unsigned long long st_d = stamp_now();
+        stamps[ct * 4 + 0] = st_tile;
+        stamps[ct * 4 + 1] = st_wait;
+        stamps[ct * 4 + 2] = st_c;
+        stamps[ct * 4 + 3] = st_d;
+      })
 #pragma unroll
       for (int i = 0; i < NA; ++i)
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       ck = 0;
       ++ct;
-      after_epi = true;
     }
     slot ^= 1;
   }
   wait_vmcnt<0>();
   wait_lgkm0();
   __builtin_amdgcn_s_barrier();
-}
-
-__device__ __forceinline__ void lds_barrier() {
-  wait_lgkm0();
-  __builtin_amdgcn_s_barrier();
+#undef SIREN_STAMP
 }
 
 }  // namespace siren

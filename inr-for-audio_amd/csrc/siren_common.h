@@ -69,6 +69,40 @@ __device__ __forceinline__ bf16x4 pack4(float a, float b, float c, float d) {
 
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 
+// 16x16 MFMA output layout -> 16-B row pieces.  A lane of 16-lane group g = lane>>4 holds 4
+// consecutive columns 4g..4g+3 (one row, lane&15) of two adjacent 16-column subtiles, a and b.
+// One v_permlane16_swap per dword (group 1 of a <-> group 0 of b, group 3 of a <-> group 2
+// of b) leaves every lane 8 consecutive columns: subtile (g&1) (a: 0, b: 1), columns
+// 8*(g>>1) .. +7 -- so a row's 32 columns go out as 4 dwordx4 instead of 8 dwordx2
+// (cdna_hip_programming.md T21, 16x16 form).  The exchange is an involution: applied to a
+// 16-B piece loaded from that position it restores the MFMA layout.
+__device__ __forceinline__ uint4 swap16_pair(uint2 a, uint2 b) {
+  const auto rx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto ry = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  return uint4{rx[0], ry[0], rx[1], ry[1]};
+}
+__device__ __forceinline__ void unswap16_pair(uint4 v, uint2& a, uint2& b) {
+  const auto rx = __builtin_amdgcn_permlane16_swap(v.x, v.z, false, false);
+  const auto ry = __builtin_amdgcn_permlane16_swap(v.y, v.w, false, false);
+  a = uint2{rx[0], ry[0]};
+  b = uint2{rx[1], ry[1]};
+}
+// column offset (in elements, from the pair's first column) of this lane's 8-column piece
+__device__ __forceinline__ int swap16_col(int lane) { return ((lane >> 4) & 1) * 16 + 8 * (lane >> 5); }
+
+__device__ __forceinline__ uint2 as_u2(bf16x4 v) { return __builtin_bit_cast(uint2, v); }
+__device__ __forceinline__ bf16x4 as_bf4(uint2 v) { return __builtin_bit_cast(bf16x4, v); }
+
+// Sum over the 16 lanes of a DPP row (lanes with equal lane>>4): fixed rotation order, result
+// in every lane of the row.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));
+  return v;
+}
+
 // Block-wide sum of one float per thread (blockDim.x multiple of 64, <= 1024).
 // `scratch` must hold blockDim.x/64 floats.  Result valid in every thread.
 __device__ __forceinline__ float block_sum(float v, float* scratch) {

@@ -29,6 +29,8 @@ struct NtParams {
   // NT_DX0 (Cprev = cos of the first layer)
   const float* t;       // [M][in]
   int in_dim;
+  int stagger;          // persistent grid: block b idles (b % 16) * stagger * ~1.7k cycles first
+  unsigned long long* stamps;  // SIREN_NT_STAMPS diagnostic builds only
 };
 
 int nt_choose_tile(int M, int N);
@@ -38,7 +40,7 @@ void gemm_tn_set_tile(int tile);
 void gemm_nt_set_pipe(int v);     // 1 = persistent 256x256 (default), 0 = one tile per block
 void gemm_tn_set_pipe(int v);     // 256x256 K-loop variant (TnL0..TnL2)
 void gemm_nt_set_grid_cap(int cap);  // persistent grid size override (0 = #CUs)
-
+void gemm_nt_set_stagger(int units); // persistent grid start stagger (see NtParams::stagger)
 struct TnParams {
   const bf16* Y;   // [R][Hin]   layer input (A role: dW column index k)
   const bf16* dZ;  // [R][Hout]  layer pre-activation gradient (B role: dW row index o)

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--tiles", default="128,256")
     ap.add_argument("--pipes", default="0,1,2", help="256x256 K-loop variants to time")
     ap.add_argument("--only", default="", help="comma list of case-name prefixes to run")
+    ap.add_argument("--staggers", default="", help="SIREN_OPT_NT_STAGGER values to add as "
+                    "extra persistent NT cases")
     args = ap.parse_args()
     import __graft_entry__ as ge
     ge.build()
@@ -94,9 +96,16 @@ def main():
     if args.only:
         pre = tuple(args.only.split(","))
         cases = {k: v for k, v in cases.items() if k.startswith(pre)}
+    stagger = {k: 0 for k in cases}
+    for v in [int(x) for x in args.staggers.split(",") if x]:
+        for k, c in list(cases.items()):
+            if v and k.endswith("p1") and not k.startswith("dw") and stagger[k] == 0:
+                cases[f"{k}_s{v}"] = c
+                stagger[f"{k}_s{v}"] = v
     times = {k: [] for k in cases}
     for _ in range(args.rounds):
         for name, (tile, pipe, fn, _) in cases.items():
+            lib.siren_set_option(5, stagger[name])
             lib.siren_set_option(0, tile if not name.startswith("dw") else 0)
             if name.startswith("dw"):
                 lib.siren_set_option(3, pipe)
@@ -111,6 +120,7 @@ def main():
             ev1.record()
             torch.cuda.synchronize()
             times[name].append(ev0.elapsed_time(ev1) / args.reps)
+    lib.siren_set_option(5, 0)
     lib.siren_set_option(0, 0)
     lib.siren_set_option(2, 1)
     lib.siren_set_option(3, 0)
