@@ -6,8 +6,12 @@
  * into the reference tree.  Conventions:
  *   - every pointer is a DEVICE pointer owned by the caller (torch allocates; the library
  *     never allocates, frees or synchronises the host);
- *   - bf16 tensors are passed as uint16_t*, row-major; fp32 weights use the nn.Linear
- *     layout [out_features][in_features];
+ *   - 16-bit tensors (activations, cosines, weight shadows, pre-activation gradients) are
+ *     IEEE fp16 passed as uint16_t*, row-major (DESIGN.md "Storage precision": fp16 keeps
+ *     the fit at the fp32 reference's quality where bf16 costs ~1.3 dB); fp32 weights use
+ *     the nn.Linear layout [out_features][in_features];
+ *   - backward pre-activation gradients dZ are stored multiplied by a power-of-two scale
+ *     S = gscale[0] (siren_grad_scale); every fp32 gradient leaves unscaled;
  *   - `stream` is a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
  *   - every function returns 0 on success, or a non-zero siren_status / hipError_t code
  *     (see siren_status_string), and never aborts the process.
@@ -22,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 1
+#define SIREN_ABI_VERSION 2
 #define SIREN_MAX_INNER 16  /* max hidden SineLayers (num_sine) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 
@@ -56,8 +60,8 @@ typedef struct siren_net {
   const float* W0;                          /* [H][in]  fp32 */
   const float* b0;                          /* [H]           */
   const float* b[SIREN_MAX_INNER];          /* [H]           */
-  const uint16_t* Wb[SIREN_MAX_INNER];      /* [H][H] bf16 shadow of W_i   */
-  const uint16_t* WTb[SIREN_MAX_INNER];     /* [H][H] bf16 shadow of W_i^T */
+  const uint16_t* Wh[SIREN_MAX_INNER];      /* [H][H] fp16 shadow of W_i   */
+  const uint16_t* WTh[SIREN_MAX_INNER];     /* [H][H] fp16 shadow of W_i^T */
   const float* w_head;                      /* [H] (net.{L+1}.weight[0])   */
   const float* b_head;                      /* [1]                          */
 } siren_net;
@@ -80,14 +84,16 @@ typedef struct siren_batch {
   int32_t zero_grads;    /* 1: zero `grads.flat` before accumulating         */
   const float* coords;   /* [rows][in]  */
   const float* target;   /* [rows]      */
-  uint16_t* Y[SIREN_MAX_INNER + 1];  /* Y[0..L] bf16 [rows][H]: layer outputs sin(.)  */
-  uint16_t* C[SIREN_MAX_INNER + 1];  /* C[0..L] bf16 [rows][H]: cos(.) of every layer  */
-  uint16_t* dZ[2];       /* bf16 [rows][H] ping-pong pre-activation gradients   */
+  uint16_t* Y[SIREN_MAX_INNER + 1];  /* Y[0..L] fp16 [rows][H]: layer outputs sin(.)  */
+  uint16_t* C[SIREN_MAX_INNER + 1];  /* C[0..L] fp16 [rows][H]: cos(.) of every layer  */
+  uint16_t* dZ[2];       /* fp16 [rows][H] ping-pong pre-activation gradients x S */
   float* out;            /* [rows] model output                                 */
   float* g;              /* [rows] dLoss/dout                                   */
   float* head_part;      /* [H/128][rows]                                       */
   float* sse_part;       /* [rows/256]                                          */
   float* gsum_part;      /* [rows/256]                                          */
+  float* gmax_part;      /* [rows/256]  max |g| per block (train / backward)    */
+  float* gscale;         /* [2]  {S, 1/S} of this micro-batch's backward        */
   float* col_part;       /* [rows/128][1+in][H]                                 */
   float* col_part2;      /* [rows/128][H]                                       */
   float* red_tmp;        /* [64][H]                                             */
@@ -107,7 +113,7 @@ int64_t siren_slab_floats(int32_t hidden, int32_t splits);
  * siren_train_step:  run.py:158-185     forward + MSELoss + loss.backward() for one
  *                    micro-batch; gradients ACCUMULATE into `grads` (global-N scaling).
  * siren_apply_update:run.py:186-187     optimizer.step() + scheduler.step(loss), then the
- *                    bf16 weight shadows are refreshed.  (`params`, `grads_flat`, `exp_avg`,
+ *                    fp16 weight shadows are refreshed.  (`params`, `grads_flat`, `exp_avg`,
  *                    `exp_avg_sq` are the flat fp32 vectors of length n_params.)          */
 int siren_forward(const siren_net* net, siren_batch* batch, void* stream);
 int siren_train_step(const siren_net* net, const siren_grads* grads, siren_batch* batch,
@@ -119,7 +125,7 @@ int siren_backward(const siren_net* net, const siren_grads* grads, siren_batch* 
 int siren_apply_update(const siren_net* net, float* params, const float* grads_flat,
                        float* exp_avg, float* exp_avg_sq, int64_t n_params,
                        float* const* W_fp32 /* [n_inner] views into params */,
-                       uint16_t* const* Wb, uint16_t* const* WTb,
+                       uint16_t* const* Wh, uint16_t* const* WTh,
                        siren_opt_state* state, const float* sse, double n_total,
                        float* loss_hist, double* lr_hist, int64_t hist_cap, void* stream);
 
@@ -127,36 +133,45 @@ int siren_apply_update(const siren_net* net, float* params, const float* grads_f
 /* utils.py:99-109 get_coord: torch.linspace(-1,1,n_total) at [offset, offset+rows) */
 int siren_coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, void* stream);
 /* models.py:114-115 first SineLayer: a0 = omega0*(t W0^T + b0) in fp32, Y0 = sin a0 and
- * C0 = cos a0 (one fp32 sincosf range reduction) -> bf16 */
+ * C0 = cos a0 (one fp32 sincosf range reduction) -> fp16 */
 int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float* b0, float omega0,
                     int32_t rows, int32_t hidden, uint16_t* Y0, uint16_t* C0, void* stream);
 /* models.py:114-115 hidden SineLayer: Y = sin(omega(X W^T + b)), C = cos(.); optional head
  * partial dot (models.py:374-381) when head_w != NULL */
-int siren_inner_fwd(const uint16_t* X, const uint16_t* Wb, const float* b, float omega, int32_t rows,
+int siren_inner_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, float omega, int32_t rows,
                     int32_t hidden, uint16_t* Y, uint16_t* C, const float* head_w, float* head_part,
                     void* stream);
-/* run.py:125,168 MSELoss + final Linear bias: out, g = 2(out-y)/n_total, partial sums */
+/* run.py:125,168 MSELoss + final Linear bias: out, g = 2(out-y)/n_total, partial sums
+ * (gmax_part may be NULL) */
 int siren_head_loss(const float* head_part, int32_t nparts, int32_t rows, const float* b_head,
                     const float* y, int32_t n_valid, double n_total, float* out, float* g,
-                    float* sse_part, float* gsum_part, void* stream);
-/* autograd of Linear(H,1) + last sin: dZ_L, db_L partials, dw_head partials */
+                    float* sse_part, float* gsum_part, float* gmax_part, void* stream);
+/* backward storage scale: gscale = {S, 1/S}, S = 2^k with max|g|*max|w_head|*omega*S < 2^6,
+ * from the nparts = rows/256 max |g| partials of siren_head_loss */
+int siren_grad_scale(const float* gmax_part, int32_t nparts, const float* w_head, int32_t hidden,
+                     float omega, float* gscale, void* stream);
+/* autograd of Linear(H,1) + last sin: dZ_L (x S), db_L partials, dw_head partials (unscaled);
+ * gscale NULL = S 1 */
 int siren_head_bwd(const uint16_t* C, const uint16_t* Y, const float* g, const float* w_head,
-                   float omega, int32_t rows, int32_t hidden, uint16_t* dZ, float* db_part,
-                   float* dwh_part, void* stream);
-/* autograd addmm dX + sin/omega backward of the layer below: dZprev = omega*cos*(dZ W) */
-int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTb, const uint16_t* Cprev, float omega_prev,
-                       int32_t rows, int32_t hidden, uint16_t* dZprev, float* db_part, void* stream);
+                   float omega, int32_t rows, int32_t hidden, const float* gscale, uint16_t* dZ,
+                   float* db_part, float* dwh_part, void* stream);
+/* autograd addmm dX + sin/omega backward of the layer below: dZprev = omega*cos*(dZ W)
+ * (carries dZ's scale); db partials multiplied by 1/S (gscale NULL = unscaled) */
+int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTh, const uint16_t* Cprev, float omega_prev,
+                       int32_t rows, int32_t hidden, const float* gscale, uint16_t* dZprev,
+                       float* db_part, void* stream);
 /* same into the fp32 first layer (C0 from siren_first_fwd): partials [rows/128][1+in][H]
- * of dZ0 and dZ0*t_j; dZ0 itself is never stored */
-int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTb1, const uint16_t* C0, const float* t,
-                       int32_t in_dim, float omega0, int32_t rows, int32_t hidden, float* part,
-                       void* stream);
+ * of dZ0 and dZ0*t_j (x 1/S); dZ0 itself is never stored */
+int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTh1, const uint16_t* C0, const float* t,
+                       int32_t in_dim, float omega0, int32_t rows, int32_t hidden, const float* gscale,
+                       float* part, void* stream);
 /* autograd addmm dW: slab[s] = partial dZ^T Y over coordinate slice s, tile edge 128/256
  * (0 = siren_dw_tile(rows, hidden)); siren_dw_reduce must get the same tile. */
 int siren_inner_bwd_dw(const uint16_t* Y, const uint16_t* dZ, int32_t rows, int32_t hidden,
                        int32_t splits, int32_t tile, float* slab, void* stream);
+/* grad (+)= (sum_s slab[s]) * gscale[1]  (gscale NULL = 1) */
 int siren_dw_reduce(const float* slab, int32_t splits, int32_t hidden, int32_t tile, float* grad,
-                    int32_t accumulate, void* stream);
+                    int32_t accumulate, const float* gscale, void* stream);
 int siren_col_reduce(const float* part, int64_t row_stride, int32_t nrows, int32_t ncols, float* out,
                      int32_t out_stride, int32_t accumulate, float* tmp, void* stream);
 /* torch.optim.Adam step over a flat fp32 vector (run.py:186) */
@@ -165,8 +180,8 @@ int siren_adam_step(float* params, const float* grads, float* exp_avg, float* ex
 /* ReduceLROnPlateau.step(loss) (run.py:187); also increments state->step */
 int siren_plateau_step(siren_opt_state* state, const float* sse, double n_total, float* loss_hist,
                        double* lr_hist, int64_t hist_cap, void* stream);
-/* bf16 shadows W and W^T of a fp32 [H_out][H_in] weight */
-int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wb, uint16_t* WTb,
+/* fp16 shadows W and W^T of a fp32 [H_out][H_in] weight */
+int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wh, uint16_t* WTh,
                       void* stream);
 
 /* ---- per-launch HIP-event profiling of the fused path (bench.py) --------------------

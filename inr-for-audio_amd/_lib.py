@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_INNER = 16
 ROW_TILE = 128
 
@@ -40,7 +40,7 @@ class SirenNet(ctypes.Structure):
         ("in_dim", _i32), ("hidden", _i32), ("n_inner", _i32), ("pad0", _i32),
         ("omega0", ctypes.c_float), ("omega", ctypes.c_float),
         ("W0", _p), ("b0", _p),
-        ("b", _p * MAX_INNER), ("Wb", _p * MAX_INNER), ("WTb", _p * MAX_INNER),
+        ("b", _p * MAX_INNER), ("Wh", _p * MAX_INNER), ("WTh", _p * MAX_INNER),
         ("w_head", _p), ("b_head", _p),
     ]
 
@@ -61,7 +61,7 @@ class SirenBatch(ctypes.Structure):
         ("coords", _p), ("target", _p),
         ("Y", _p * (MAX_INNER + 1)), ("C", _p * (MAX_INNER + 1)), ("dZ", _p * 2),
         ("out", _p), ("g", _p), ("head_part", _p), ("sse_part", _p), ("gsum_part", _p),
-        ("col_part", _p), ("col_part2", _p), ("red_tmp", _p), ("slab", _p),
+        ("gmax_part", _p), ("gscale", _p), ("col_part", _p), ("col_part2", _p), ("red_tmp", _p), ("slab", _p),
     ]
 
 
@@ -84,12 +84,14 @@ _SIGS = {
     "siren_first_fwd": (ctypes.c_int, [_p, _i32, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p]),
     "siren_inner_fwd": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p]),
     "siren_head_loss": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _i32, ctypes.c_double, _p, _p, _p, _p,
-                                       _p]),
-    "siren_head_bwd": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p]),
-    "siren_inner_bwd_dx": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p]),
-    "siren_first_bwd_dx": (ctypes.c_int, [_p, _p, _p, _p, _i32, ctypes.c_float, _i32, _i32, _p, _p]),
+                                       _p, _p]),
+    "siren_grad_scale": (ctypes.c_int, [_p, _i32, _p, _i32, ctypes.c_float, _p, _p]),
+    "siren_head_bwd": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p]),
+    "siren_inner_bwd_dx": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p]),
+    "siren_first_bwd_dx": (ctypes.c_int, [_p, _p, _p, _p, _i32, ctypes.c_float, _i32, _i32, _p, _p,
+                                          _p]),
     "siren_inner_bwd_dw": (ctypes.c_int, [_p, _p, _i32, _i32, _i32, _i32, _p, _p]),
-    "siren_dw_reduce": (ctypes.c_int, [_p, _i32, _i32, _i32, _p, _i32, _p]),
+    "siren_dw_reduce": (ctypes.c_int, [_p, _i32, _i32, _i32, _p, _i32, _p, _p]),
     "siren_nt_tile": (_i32, [_i32, _i32]),
     "siren_dw_tile": (_i32, [_i32, _i32]),
     "siren_col_reduce": (ctypes.c_int, [_p, _i64, _i32, _i32, _p, _i32, _i32, _p, _p]),

@@ -12,8 +12,8 @@ static_assert(sizeof(siren_opt_state) == sizeof(OptState), "opt state layout");
 namespace {
 
 inline hipStream_t S(void* s) { return (hipStream_t)s; }
-inline const bf16* B(const uint16_t* p) { return (const bf16*)p; }
-inline bf16* B(uint16_t* p) { return (bf16*)p; }
+inline const h16* B(const uint16_t* p) { return (const h16*)p; }
+inline h16* B(uint16_t* p) { return (h16*)p; }
 
 #define SIREN_TRY(expr)                        \
   do {                                         \
@@ -58,7 +58,7 @@ int check_net(const siren_net* n) {
   if (n->n_inner < 1 || n->n_inner > SIREN_MAX_INNER) return SIREN_ERR_CONFIG;
   if (!n->W0 || !n->b0 || !n->w_head || !n->b_head) return SIREN_ERR_NULL;
   for (int i = 0; i < n->n_inner; ++i)
-    if (!n->b[i] || !n->Wb[i] || !n->WTb[i]) return SIREN_ERR_NULL;
+    if (!n->b[i] || !n->Wh[i] || !n->WTh[i]) return SIREN_ERR_NULL;
   return SIREN_OK;
 }
 
@@ -72,7 +72,7 @@ int check_batch(const siren_net* n, const siren_batch* b, bool train) {
     if (!b->Y[i] || !b->C[i]) return SIREN_ERR_NULL;
   if (train) {
     if (!b->target || !b->dZ[0] || !b->dZ[1] || !b->col_part || !b->col_part2 || !b->red_tmp ||
-        !b->slab)
+        !b->slab || !b->gmax_part || !b->gscale)
       return SIREN_ERR_NULL;
     if (b->splits < 1 || b->n_total <= 0) return SIREN_ERR_CONFIG;
   }
@@ -87,7 +87,7 @@ hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s) {
   for (int i = 0; i < L; ++i) {
     NtParams p = {};
     p.X = B(b->Y[i]);
-    p.W = B(n->Wb[i]);
+    p.W = B(n->Wh[i]);
     p.M = R; p.N = H; p.K = H;
     p.tile = nt_choose_tile(R, H);
     p.omega = n->omega;
@@ -147,7 +147,7 @@ int siren_forward(const siren_net* net, siren_batch* batch, void* stream) {
   // out = sum of head partials + bias (g/sse unused at inference: n_valid = 0 path)
   SIREN_TRY(head_loss(batch->head_part, net->hidden / nt_choose_tile(batch->rows, net->hidden),
                       batch->rows, net->b_head, batch->out,
-                      0, 0.f, batch->out, batch->g, batch->sse_part, batch->gsum_part, s));
+                      0, 0.f, batch->out, batch->g, batch->sse_part, batch->gsum_part, nullptr, s));
   return SIREN_OK;
 }
 
@@ -163,8 +163,10 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
   const int R = b->rows, H = net->hidden, L = net->n_inner, in = net->in_dim;
   const int ntile = nt_choose_tile(R, H), tntile = tn_choose_tile(R, H, H);
   const int prow = R / ntile;  // partial rows written by the NT_DX / NT_DX0 epilogues
+  SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale(b->gmax_part, (R + 255) / 256, net->w_head, H, net->omega,
+                                            b->gscale, s));
   SIREN_PROF(SIREN_PROF_HEAD, s, head_bwd(B(b->C[L]), B(b->Y[L]), b->g, net->w_head, net->omega, R, H,
-                                          B(b->dZ[0]), b->col_part, b->col_part2, s));
+                                          b->gscale, B(b->dZ[0]), b->col_part, b->col_part2, s));
   SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part2, H, R / 128, H, gr->w_head, 1, 1, b->red_tmp, s));
   SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, R / 128, H, gr->b[L - 1], 1, 1, b->red_tmp, s));
 
@@ -178,14 +180,16 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
     tp.tile = tntile;
     tp.slab = b->slab;
     SIREN_PROF(SIREN_PROF_BWD_DW, s, gemm_tn_dw(tp, s));
-    SIREN_PROF(SIREN_PROF_REDUCE, s, dw_reduce(b->slab, b->splits, H, H, tntile, gr->W[i], 1, s));
+    SIREN_PROF(SIREN_PROF_REDUCE, s, dw_reduce(b->slab, b->splits, H, H, tntile, gr->W[i], 1,
+                                                       b->gscale, s));
 
     NtParams p = {};
     p.X = B(b->dZ[cur]);
-    p.W = B(net->WTb[i]);
+    p.W = B(net->WTh[i]);
     p.M = R; p.N = H; p.K = H;
     p.tile = ntile;
     p.colsum_part = b->col_part;
+    p.gscale = b->gscale;
     if (i > 0) {
       p.omega = net->omega;
       p.Cprev = B(b->C[i]);
@@ -222,10 +226,10 @@ int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b
 
   // ---- forward (models.py:388-394) + MSE (run.py:168) ----
   SIREN_TRY(run_forward(net, b, s));
-  const float gscale = (float)(2.0 / b->n_total);  // MSELoss mean backward: 2/N
+  const float gfac = (float)(2.0 / b->n_total);  // MSELoss mean backward: 2/N
   SIREN_PROF(SIREN_PROF_HEAD, s, head_loss(b->head_part, H / nt_choose_tile(R, H), R, net->b_head,
-                                           b->target, b->n_valid,
-                                           gscale, b->out, b->g, b->sse_part, b->gsum_part, s));
+                                           b->target, b->n_valid, gfac, b->out, b->g, b->sse_part,
+                                           b->gsum_part, b->gmax_part, s));
   const int nsum = (R + 255) / 256;
   SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->sse_part, nsum, gr->sse, 1, s));
   SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->gsum_part, nsum, gr->b_head, 1, s));
@@ -240,24 +244,25 @@ int siren_backward(const siren_net* net, const siren_grads* gr, siren_batch* b, 
   if ((st = check_grads(net, gr))) return st;
   hipStream_t s = S(stream);
   if (b->zero_grads && gr->flat) SIREN_TRY(hipMemsetAsync(gr->flat, 0, gr->flat_len * sizeof(float), s));
-  // bias of the head: sum of g (gsum_part reused as scratch)
+  // bias of the head: sum of g; max |g| partials for the backward storage scale
   SIREN_TRY(sum_to(b->g, b->rows, gr->b_head, 1, s));
+  SIREN_TRY(gmax_partials(b->g, b->rows, b->gmax_part, s));
   return run_backward(net, gr, b, s);
 }
 
 int siren_apply_update(const siren_net* net, float* params, const float* grads_flat, float* exp_avg,
-                       float* exp_avg_sq, int64_t n_params, float* const* W_fp32, uint16_t* const* Wb,
-                       uint16_t* const* WTb, siren_opt_state* state, const float* sse, double n_total,
+                       float* exp_avg_sq, int64_t n_params, float* const* W_fp32, uint16_t* const* Wh,
+                       uint16_t* const* WTh, siren_opt_state* state, const float* sse, double n_total,
                        float* loss_hist, double* lr_hist, int64_t hist_cap, void* stream) {
   int st = check_net(net);
   if (st) return st;
-  if (!params || !grads_flat || !exp_avg || !exp_avg_sq || !state || !sse || !W_fp32 || !Wb || !WTb)
+  if (!params || !grads_flat || !exp_avg || !exp_avg_sq || !state || !sse || !W_fp32 || !Wh || !WTh)
     return SIREN_ERR_NULL;
   hipStream_t s = S(stream);
   SIREN_PROF(SIREN_PROF_UPDATE, s, adam_flat(params, grads_flat, exp_avg, exp_avg_sq, n_params,
                                              (const OptState*)state, s));
   for (int i = 0; i < net->n_inner; ++i)
-    SIREN_PROF(SIREN_PROF_UPDATE, s, cast_weight(W_fp32[i], net->hidden, net->hidden, B(Wb[i]), B(WTb[i]), s));
+    SIREN_PROF(SIREN_PROF_UPDATE, s, cast_weight(W_fp32[i], net->hidden, net->hidden, B(Wh[i]), B(WTh[i]), s));
   SIREN_PROF(SIREN_PROF_UPDATE, s, plateau_step((OptState*)state, sse, n_total, loss_hist, lr_hist, hist_cap, s));
   return SIREN_OK;
 }
@@ -278,14 +283,14 @@ int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float
   return (int)first_fwd(t, in_dim, W0, b0, omega0, rows, hidden, B(Y0), B(C0), S(stream));
 }
 
-int siren_inner_fwd(const uint16_t* X, const uint16_t* Wb, const float* b, float omega, int32_t rows,
+int siren_inner_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, float omega, int32_t rows,
                     int32_t hidden, uint16_t* Y, uint16_t* C, const float* head_w, float* head_part,
                     void* stream) {
-  if (!X || !Wb || !b || !Y || !C) return SIREN_ERR_NULL;
+  if (!X || !Wh || !b || !Y || !C) return SIREN_ERR_NULL;
   if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
   if (head_w && !head_part) return SIREN_ERR_NULL;
   NtParams p = {};
-  p.X = B(X); p.W = B(Wb); p.M = rows; p.N = hidden; p.K = hidden;
+  p.X = B(X); p.W = B(Wh); p.M = rows; p.N = hidden; p.K = hidden;
   p.tile = nt_choose_tile(rows, hidden);
   p.omega = omega; p.bias = b; p.Y = B(Y); p.C = B(C);
   p.head_w = head_w; p.head_part = head_part;
@@ -294,44 +299,54 @@ int siren_inner_fwd(const uint16_t* X, const uint16_t* Wb, const float* b, float
 
 int siren_head_loss(const float* head_part, int32_t nparts, int32_t rows, const float* b_head,
                     const float* y, int32_t n_valid, double n_total, float* out, float* g,
-                    float* sse_part, float* gsum_part, void* stream) {
+                    float* sse_part, float* gsum_part, float* gmax_part, void* stream) {
   if (!head_part || !b_head || !out || !g || !sse_part || !gsum_part) return SIREN_ERR_NULL;
   if (n_valid > 0 && !y) return SIREN_ERR_NULL;
   if (rows <= 0 || nparts < 1 || n_valid > rows || n_total <= 0) return SIREN_ERR_SHAPE;
   return (int)head_loss(head_part, nparts, rows, b_head, y, n_valid, (float)(2.0 / n_total), out, g,
-                        sse_part, gsum_part, S(stream));
+                        sse_part, gsum_part, gmax_part, S(stream));
+}
+
+int siren_grad_scale(const float* gmax_part, int32_t nparts, const float* w_head, int32_t hidden,
+                     float omega, float* gscale, void* stream) {
+  if (!gmax_part || !w_head || !gscale) return SIREN_ERR_NULL;
+  if (nparts < 1 || hidden < 1) return SIREN_ERR_SHAPE;
+  return (int)grad_scale(gmax_part, nparts, w_head, hidden, omega, gscale, S(stream));
 }
 
 int siren_head_bwd(const uint16_t* C, const uint16_t* Y, const float* g, const float* w_head,
-                   float omega, int32_t rows, int32_t hidden, uint16_t* dZ, float* db_part,
-                   float* dwh_part, void* stream) {
+                   float omega, int32_t rows, int32_t hidden, const float* gscale, uint16_t* dZ,
+                   float* db_part, float* dwh_part, void* stream) {
   if (!C || !Y || !g || !w_head || !dZ || !db_part || !dwh_part) return SIREN_ERR_NULL;
   if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
-  return (int)head_bwd(B(C), B(Y), g, w_head, omega, rows, hidden, B(dZ), db_part, dwh_part,
+  return (int)head_bwd(B(C), B(Y), g, w_head, omega, rows, hidden, gscale, B(dZ), db_part, dwh_part,
                        S(stream));
 }
 
-int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTb, const uint16_t* Cprev, float omega_prev,
-                       int32_t rows, int32_t hidden, uint16_t* dZprev, float* db_part, void* stream) {
-  if (!dZ || !WTb || !Cprev || !dZprev || !db_part) return SIREN_ERR_NULL;
+int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTh, const uint16_t* Cprev, float omega_prev,
+                       int32_t rows, int32_t hidden, const float* gscale, uint16_t* dZprev,
+                       float* db_part, void* stream) {
+  if (!dZ || !WTh || !Cprev || !dZprev || !db_part) return SIREN_ERR_NULL;
   if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
   NtParams p = {};
-  p.X = B(dZ); p.W = B(WTb); p.M = rows; p.N = hidden; p.K = hidden;
+  p.X = B(dZ); p.W = B(WTh); p.M = rows; p.N = hidden; p.K = hidden;
   p.tile = nt_choose_tile(rows, hidden);
   p.omega = omega_prev; p.Cprev = B(Cprev); p.dZ = B(dZprev); p.colsum_part = db_part;
+  p.gscale = gscale;
   return (int)gemm_nt(NT_DX, false, p, S(stream));
 }
 
-int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTb1, const uint16_t* C0, const float* t,
-                       int32_t in_dim, float omega0, int32_t rows, int32_t hidden, float* part,
-                       void* stream) {
-  if (!dZ1 || !WTb1 || !C0 || !t || !part) return SIREN_ERR_NULL;
+int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTh1, const uint16_t* C0, const float* t,
+                       int32_t in_dim, float omega0, int32_t rows, int32_t hidden, const float* gscale,
+                       float* part, void* stream) {
+  if (!dZ1 || !WTh1 || !C0 || !t || !part) return SIREN_ERR_NULL;
   if (in_dim < 1 || in_dim > 2) return SIREN_ERR_CONFIG;
   if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
   NtParams p = {};
-  p.X = B(dZ1); p.W = B(WTb1); p.M = rows; p.N = hidden; p.K = hidden;
+  p.X = B(dZ1); p.W = B(WTh1); p.M = rows; p.N = hidden; p.K = hidden;
   p.tile = nt_choose_tile(rows, hidden);
   p.omega = omega0; p.Cprev = B(C0); p.t = t; p.in_dim = in_dim; p.colsum_part = part;
+  p.gscale = gscale;
   return (int)gemm_nt(NT_DX0, false, p, S(stream));
 }
 
@@ -348,11 +363,11 @@ int siren_inner_bwd_dw(const uint16_t* Y, const uint16_t* dZ, int32_t rows, int3
 }
 
 int siren_dw_reduce(const float* slab, int32_t splits, int32_t hidden, int32_t tile, float* grad,
-                    int32_t accumulate, void* stream) {
+                    int32_t accumulate, const float* gscale, void* stream) {
   if (!slab || !grad) return SIREN_ERR_NULL;
   if (!hidden_ok(hidden) || splits < 1) return SIREN_ERR_SHAPE;
   if (tile != 128 && tile != 256) return SIREN_ERR_CONFIG;
-  return (int)dw_reduce(slab, splits, hidden, hidden, tile, grad, accumulate, S(stream));
+  return (int)dw_reduce(slab, splits, hidden, hidden, tile, grad, accumulate, gscale, S(stream));
 }
 
 int siren_col_reduce(const float* part, int64_t row_stride, int32_t nrows, int32_t ncols, float* out,
@@ -376,11 +391,11 @@ int siren_plateau_step(siren_opt_state* state, const float* sse, double n_total,
   return (int)plateau_step((OptState*)state, sse, n_total, loss_hist, lr_hist, hist_cap, S(stream));
 }
 
-int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wb, uint16_t* WTb,
+int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wh, uint16_t* WTh,
                       void* stream) {
-  if (!W || !Wb || !WTb) return SIREN_ERR_NULL;
+  if (!W || !Wh || !WTh) return SIREN_ERR_NULL;
   if (h_out % 64 || h_in % 64) return SIREN_ERR_SHAPE;
-  return (int)cast_weight(W, h_out, h_in, B(Wb), B(WTb), S(stream));
+  return (int)cast_weight(W, h_out, h_in, B(Wh), B(WTh), S(stream));
 }
 
 int siren_set_option(int32_t option, int32_t value) {

@@ -1,5 +1,5 @@
 // Memory-bound SIREN kernels: coordinate grid, fp32 first layer, head/MSE, column
-// reductions, fused Adam, ReduceLROnPlateau and the bf16 weight shadows.
+// reductions, fused Adam, ReduceLROnPlateau and the h16 weight shadows.
 #include <math.h>
 #include "siren_common.h"
 #include "siren_kernels.h"
@@ -45,7 +45,7 @@ hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, 
 // K=2: fma(t1, w1, t0*w0) + b) and sinf does a full-precision range reduction.
 __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const float* __restrict__ W0,
                                  const float* __restrict__ b0, float omega0, int R, int H,
-                                 bf16* __restrict__ Y0, bf16* __restrict__ C0) {
+                                 h16* __restrict__ Y0, h16* __restrict__ C0) {
   const int hq = H >> 2;
   const int64_t total = (int64_t)R * hq;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
@@ -62,13 +62,13 @@ __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const 
       else z = __builtin_fmaf(t1, W0[(n + r) * 2 + 1], t0 * W0[(n + r) * 2]) + b0[n + r];
       sincosf(omega0 * z, &y[r], &c[r]);
     }
-    *(bf16x4*)(Y0 + m * H + n) = pack4(y[0], y[1], y[2], y[3]);
-    *(bf16x4*)(C0 + m * H + n) = pack4(c[0], c[1], c[2], c[3]);
+    *(h16x4*)(Y0 + m * H + n) = pack4(y[0], y[1], y[2], y[3]);
+    *(h16x4*)(C0 + m * H + n) = pack4(c[0], c[1], c[2], c[3]);
   }
 }
 
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
-                     int R, int H, bf16* Y0, bf16* C0, hipStream_t s) {
+                     int R, int H, h16* Y0, h16* C0, hipStream_t s) {
   if (H % 4 || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
   hipLaunchKernelGGL(first_fwd_kernel, dim3(grid_for((int64_t)R * (H / 4), 256)), dim3(256), 0, s, t,
                      in_dim, W0, b0, omega0, R, H, Y0, C0);
@@ -78,12 +78,13 @@ hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b
 // ---------------------------------------------------------------------------------
 // Final nn.Linear(H,1) + MSELoss (models.py:374-381, run.py:125,168):
 //   out = sum_j head_part[j][m] + b;  err = out - y;  g = err * (2/N_total) (0 on pad rows)
-// plus per-block partial sums of err^2 (loss) and g (bias gradient).
+// plus per-block partial sums of err^2 (loss) and g (bias gradient), and per-block max |g|
+// (for grad_scale).
 __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts, int R,
                                  const float* __restrict__ b_head, const float* __restrict__ y,
-                                 int n_valid, float gscale, float* __restrict__ out,
+                                 int n_valid, float gfac, float* __restrict__ out,
                                  float* __restrict__ g, float* __restrict__ sse_part,
-                                 float* __restrict__ gsum_part) {
+                                 float* __restrict__ gsum_part, float* __restrict__ gmax_part) {
   __shared__ float scratch[4];
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   float e2 = 0.f, gv = 0.f;
@@ -95,23 +96,76 @@ __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts
     if (m < n_valid) {
       const float err = o - y[m];
       e2 = err * err;
-      gv = err * gscale;
+      gv = err * gfac;
     }
     g[m] = gv;
   }
   const float se = block_sum(e2, scratch);
   const float gs = block_sum(gv, scratch);
+  const float gm = block_max(fabsf(gv), scratch);
   if (threadIdx.x == 0) {
     sse_part[blockIdx.x] = se;
     gsum_part[blockIdx.x] = gs;
+    if (gmax_part) gmax_part[blockIdx.x] = gm;
   }
 }
 
 hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_head, const float* y,
-                     int n_valid, float gscale, float* out, float* g, float* sse_part,
-                     float* gsum_part, hipStream_t s) {
+                     int n_valid, float gfac, float* out, float* g, float* sse_part,
+                     float* gsum_part, float* gmax_part, hipStream_t s) {
   hipLaunchKernelGGL(head_loss_kernel, dim3((R + 255) / 256), dim3(256), 0, s, head_part, nparts, R,
-                     b_head, y, n_valid, gscale, out, g, sse_part, gsum_part);
+                     b_head, y, n_valid, gfac, out, g, sse_part, gsum_part, gmax_part);
+  return hipGetLastError();
+}
+
+// Per-256-row-block max |g| of an externally supplied dLoss/dout (siren_backward).
+__global__ void gmax_partials_kernel(const float* __restrict__ g, int R, float* __restrict__ gmax_part) {
+  __shared__ float scratch[4];
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  const float gm = block_max(m < R ? fabsf(g[m]) : 0.f, scratch);
+  if (threadIdx.x == 0) gmax_part[blockIdx.x] = gm;
+}
+
+hipError_t gmax_partials(const float* g, int R, float* gmax_part, hipStream_t s) {
+  hipLaunchKernelGGL(gmax_partials_kernel, dim3((R + 255) / 256), dim3(256), 0, s, g, R, gmax_part);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// Backward gradient scale.  dZ is stored in fp16 (11-bit significand, the precision the
+// forward needs -- DESIGN.md "Storage precision"), whose exponent range cannot hold raw
+// MSE gradients (|g| ~ 2|err|/N reaches 1e-9 at N = 2^20).  The head backward therefore
+// stores dZ * S with S = 2^k chosen so that its bound max|g| * max|w_head| * omega lands
+// just under 2^6 (headroom for growth through the layers below), and every fp32 gradient
+// reduced from a scaled dZ is multiplied by 1/S.  Powers of two: scaling is exact.
+// gscale[0] = S, gscale[1] = 1/S.  One block.
+__global__ void grad_scale_kernel(const float* __restrict__ gmax_part, int nparts,
+                                  const float* __restrict__ w_head, int H, float omega,
+                                  float* __restrict__ gscale) {
+  __shared__ float scratch[4];
+  float gm = 0.f, wm = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) gm = fmaxf(gm, gmax_part[i]);
+  for (int i = threadIdx.x; i < H; i += blockDim.x) wm = fmaxf(wm, fabsf(w_head[i]));
+  gm = block_max(gm, scratch);
+  wm = block_max(wm, scratch);
+  if (threadIdx.x == 0) {
+    const float bound = gm * wm * fabsf(omega);
+    int k = 0;
+    if (bound > 0.f && bound < INFINITY) {
+      int e;
+      (void)frexpf(bound, &e);  // bound < 2^e
+      k = 6 - e;
+      k = k < -100 ? -100 : (k > 100 ? 100 : k);
+    }
+    gscale[0] = ldexpf(1.0f, k);
+    gscale[1] = ldexpf(1.0f, -k);
+  }
+}
+
+hipError_t grad_scale(const float* gmax_part, int nparts, const float* w_head, int H, float omega,
+                      float* gscale, hipStream_t s) {
+  hipLaunchKernelGGL(grad_scale_kernel, dim3(1), dim3(256), 0, s, gmax_part, nparts, w_head, H, omega,
+                     gscale);
   return hipGetLastError();
 }
 
@@ -119,11 +173,14 @@ hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_h
 // Backward through the head into the last hidden SineLayer:
 //   dY[m][n] = g[m]*w[n];  dZ = (dY * cos) * omega;  db partial = sum_m dZ;
 //   dw_head partial = sum_m g[m]*Y[m][n].     One block per 128 rows.
-__global__ void head_bwd_kernel(const bf16* __restrict__ C, const bf16* __restrict__ Y,
+// The partials are unscaled; the stored dZ carries the gradient scale S (grad_scale).
+__global__ void head_bwd_kernel(const h16* __restrict__ C, const h16* __restrict__ Y,
                                 const float* __restrict__ g, const float* __restrict__ w_head,
-                                float omega, int R, int H, bf16* __restrict__ dZ,
-                                float* __restrict__ db_part, float* __restrict__ dwh_part) {
+                                float omega, int R, int H, const float* __restrict__ gscale,
+                                h16* __restrict__ dZ, float* __restrict__ db_part,
+                                float* __restrict__ dwh_part) {
   __shared__ float red[2][256 * 4];
+  const float S = gscale ? gscale[0] : 1.0f;  // dZ storage scale (grad_scale)
   const int hq = H >> 2;            // column quads (divides 256)
   const int cq = threadIdx.x % hq, rg = threadIdx.x / hq, nrg = blockDim.x / hq;
   const int n = cq * 4;
@@ -134,8 +191,8 @@ __global__ void head_bwd_kernel(const bf16* __restrict__ C, const bf16* __restri
   for (int r = rg; r < 128; r += nrg) {
     const int64_t m = m0 + r;
     const float gm = g[m];
-    const bf16x4 c = *(const bf16x4*)(C + m * H + n);
-    const bf16x4 yv = *(const bf16x4*)(Y + m * H + n);
+    const h16x4 c = *(const h16x4*)(C + m * H + n);
+    const h16x4 yv = *(const h16x4*)(Y + m * H + n);
     float dz[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -143,7 +200,7 @@ __global__ void head_bwd_kernel(const bf16* __restrict__ C, const bf16* __restri
       db[k] += dz[k];
       dw[k] += gm * (float)yv[k];
     }
-    *(bf16x4*)(dZ + m * H + n) = pack4(dz[0], dz[1], dz[2], dz[3]);
+    *(h16x4*)(dZ + m * H + n) = pack4(dz[0] * S, dz[1] * S, dz[2] * S, dz[3] * S);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -163,11 +220,12 @@ __global__ void head_bwd_kernel(const bf16* __restrict__ C, const bf16* __restri
   }
 }
 
-hipError_t head_bwd(const bf16* C, const bf16* Y, const float* g, const float* w_head, float omega,
-                    int R, int H, bf16* dZ, float* db_part, float* dwh_part, hipStream_t s) {
+hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_head, float omega,
+                    int R, int H, const float* gscale, h16* dZ, float* db_part, float* dwh_part,
+                    hipStream_t s) {
   if (R % 128 || H % 4 || 256 % (H / 4)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(head_bwd_kernel, dim3(R / 128), dim3(256), 0, s, C, Y, g, w_head, omega, R, H,
-                     dZ, db_part, dwh_part);
+                     gscale, dZ, db_part, dwh_part);
   return hipGetLastError();
 }
 
@@ -305,23 +363,23 @@ hipError_t plateau_step(OptState* st, const float* sse, double n_total, float* l
 }
 
 // ---------------------------------------------------------------------------------
-// bf16 shadows of a hidden weight W[o][k] (fp32 master): Wb = W, WTb = W^T, through a
+// h16 shadows of a hidden weight W[o][k] (fp32 master): Wb = W, WTb = W^T, through a
 // 64x64 LDS transpose so both stores are coalesced.
 __global__ void cast_weight_kernel(const float* __restrict__ W, int H_out, int H_in,
-                                   bf16* __restrict__ Wb, bf16* __restrict__ WTb) {
+                                   h16* __restrict__ Wb, h16* __restrict__ WTb) {
   __shared__ float tile[64][65];
   const int o0 = blockIdx.y * 64, k0 = blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: 64 x 4
   for (int r = ty; r < 64; r += 4) {
     const float w = W[(size_t)(o0 + r) * H_in + k0 + tx];
     tile[r][tx] = w;
-    Wb[(size_t)(o0 + r) * H_in + k0 + tx] = (bf16)w;
+    Wb[(size_t)(o0 + r) * H_in + k0 + tx] = (h16)w;
   }
   __syncthreads();
-  for (int r = ty; r < 64; r += 4) WTb[(size_t)(k0 + r) * H_out + o0 + tx] = (bf16)tile[tx][r];
+  for (int r = ty; r < 64; r += 4) WTb[(size_t)(k0 + r) * H_out + o0 + tx] = (h16)tile[tx][r];
 }
 
-hipError_t cast_weight(const float* W, int H_out, int H_in, bf16* Wb, bf16* WTb, hipStream_t s) {
+hipError_t cast_weight(const float* W, int H_out, int H_in, h16* Wb, h16* WTb, hipStream_t s) {
   if (H_out % 64 || H_in % 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(cast_weight_kernel, dim3(H_in / 64, H_out / 64), dim3(256), 0, s, W, H_out, H_in,
                      Wb, WTb);

@@ -1,17 +1,17 @@
-// NT GEMM for the SIREN hidden layers on gfx950 bf16 MFMA with fused epilogues.
+// NT GEMM for the SIREN hidden layers on gfx950 h16 MFMA with fused epilogues.
 //
-//   acc[m][n] = sum_k X[m][k] * W[n][k]        (X: [M][K] bf16, W: [N][K] bf16, fp32 acc)
+//   acc[m][n] = sum_k X[m][k] * W[n][k]        (X: [M][K] h16, W: [N][K] h16, fp32 acc)
 //
 // Three epilogues (template MODE):
-//   NT_FWD : a = omega*(acc + b[n]);  Y = sin a, C = cos a   (bf16 out)     -- models.py:114-115
+//   NT_FWD : a = omega*(acc + b[n]);  Y = sin a, C = cos a   (h16 out)     -- models.py:114-115
 //            optional HEAD: per-row partial of sum_n Y[m][n]*w_head[n]      -- models.py:374-381
-//   NT_DX  : dz = (acc * Cprev[m][n]) * omega_prev  (bf16 out) + column partial sums (db)
+//   NT_DX  : dz = (acc * Cprev[m][n]) * omega_prev  (h16 out) + column partial sums (db)
 //            = autograd of sin(omega*linear) for the layer below            -- models.py:114-115
 //   NT_DX0 : same, into the fp32 first layer (Cprev = its cos from first_fwd): only the
 //            column partial sums of dz and dz*t_j (db0, dW0) are written; dZ0 never
 //            reaches HBM.
 //
-// Tiles: 256x256 with 8 waves (2x4, each 128x64 = 8x4 v_mfma_f32_16x16x32_bf16 tiles),
+// Tiles: 256x256 with 8 waves (2x4, each 128x64 = 8x4 v_mfma_f32_16x16x32_f16 tiles),
 // PERSISTENT: one block per CU walks its tiles and the double-buffered LDS ring runs across
 // tile boundaries (gemm_pipeline.h mfma_pipeline_tiles): both first operand stages of tile
 // i+1 are in flight before tile i's epilogue issues its stores, which then drain under
@@ -33,7 +33,7 @@
 
 namespace siren {
 
-// Source-side XOR swizzle of a staged [rows][64] bf16 image (128-B rows, 8 16-B chunks).
+// Source-side XOR swizzle of a staged [rows][64] h16 image (128-B rows, 8 16-B chunks).
 __device__ __forceinline__ int stage_swz(int r, int c) { return c ^ (r & 7); }
 
 template <int BM_, int BN_, int WM_, int WN_>
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     tile_of(ti, m0, n0);
     const char* xs = smem + slot * Cfg::STAGE + wave * Cfg::XINSTR * 1024;
     const char* ws = smem + slot * Cfg::STAGE + Cfg::XBYTES + wave * Cfg::WINSTR * 1024;
-    const bf16* xk = p.X + (size_t)m0 * K + kt * BK;
-    const bf16* wk = p.W + (size_t)n0 * K + kt * BK;
+    const h16* xk = p.X + (size_t)m0 * K + kt * BK;
+    const h16* wk = p.W + (size_t)n0 * K + kt * BK;
 #pragma unroll
     for (int j = 0; j < Cfg::XINSTR; ++j) glds16_asm(xk + xrel[j], lds_addr(xs + j * 1024));
 #pragma unroll
@@ -130,13 +130,13 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
     koff[kk] = (lane & 15) * ROWB + (stage_swz(lane & 15, (lane >> 4) + 4 * kk) << 4);
-  auto frags = [&](int slot, int kk, bf16x8 (&A)[SN], bf16x8 (&B)[SM]) {
+  auto frags = [&](int slot, int kk, h16x8 (&A)[SN], h16x8 (&B)[SM]) {
     const char* xs = smem + slot * Cfg::STAGE;
     const char* ws = xs + Cfg::XBYTES;
 #pragma unroll
-    for (int i = 0; i < SN; ++i) A[i] = *(const bf16x8*)(ws + (wn * TN + i * 16) * ROWB + koff[kk]);
+    for (int i = 0; i < SN; ++i) A[i] = *(const h16x8*)(ws + (wn * TN + i * 16) * ROWB + koff[kk]);
 #pragma unroll
-    for (int j = 0; j < SM; ++j) B[j] = *(const bf16x8*)(xs + (wm * TM + j * 16) * ROWB + koff[kk]);
+    for (int j = 0; j < SM; ++j) B[j] = *(const h16x8*)(xs + (wm * TM + j * 16) * ROWB + koff[kk]);
   };
 
   f32x4 acc[SN][SM];
@@ -162,6 +162,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     }
     // visible to other waves after the pipeline's first barrier
   }
+  // dZ carries the backward storage scale S; the fp32 column partials leave unscaled
+  const float inv_scale = (MODE != NT_FWD && p.gscale) ? p.gscale[1] : 1.0f;
   // NT_DX / NT_DX0 epilogue operands loaded by `pre` (before the next tile's early prefetch)
   constexpr int PRE_J = (MODE == NT_FWD) ? 0 : (MODE == NT_DX ? SM : SM / 2);
   uint4 cp_in[PRE_J > 0 ? PRE_J : 1][SN / 2];
@@ -287,7 +289,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int i = 2 * pp + h;
-            const bf16x4 cp = as_bf4(cpu[h]);
+            const h16x4 cp = as_h4(cpu[h]);
             float dz[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           float s = 0.f;
 #pragma unroll
           for (int w = 0; w < Cfg::WM; ++w) s += red[(q * Cfg::WM + w) * BN + tid];
-          p.colsum_part[((size_t)tm * nred + q) * N + n0 + tid] = s;
+          p.colsum_part[((size_t)tm * nred + q) * N + n0 + tid] = s * inv_scale;
         }
       }
     }

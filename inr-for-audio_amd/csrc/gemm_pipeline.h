@@ -38,13 +38,13 @@ __device__ __forceinline__ void mfma_pipeline(int nk, f32x4 (&acc)[NA][NB], Stag
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) stage(s, s);
 
-  auto mma = [&](bf16x8 (&A)[NA], bf16x8 (&B)[NB]) {
+  auto mma = [&](h16x8 (&A)[NA], h16x8 (&B)[NB]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < NA; ++i)
 #pragma unroll
       for (int j = 0; j < NB; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[i], B[j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -58,7 +58,7 @@ __device__ __forceinline__ void mfma_pipeline(int nk, f32x4 (&acc)[NA][NB], Stag
       if (t + S - 1 < nk) stage(t + S - 1, fill);
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        bf16x8 A[NA], B[NB];
+        h16x8 A[NA], B[NB];
         frags(slot, kk, A, B);
         mma(A, B);
       }
@@ -71,7 +71,7 @@ __device__ __forceinline__ void mfma_pipeline(int nk, f32x4 (&acc)[NA][NB], Stag
     if (S - 2 < nk) wait_vmcnt<G * (S - 2)>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    bf16x8 A0[NA], B0[NB], A1[NA], B1[NB];
+    h16x8 A0[NA], B0[NB], A1[NA], B1[NB];
     frags(0, 0, A0, B0);
     int slot = 0, fill = S - 1;
     for (int t = 0; t < nk; t += 2) {
@@ -182,13 +182,13 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      bf16x8 A[NA], B[NB];
+      h16x8 A[NA], B[NB];
       frags(slot, kk, A, B);
 #pragma unroll
       for (int i = 0; i < NA; ++i)
 #pragma unroll
         for (int j = 0; j < NB; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[i], B[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[i], B[j], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
     after = (after == 1) ? 2 : 0;

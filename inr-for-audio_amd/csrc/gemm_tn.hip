@@ -1,4 +1,4 @@
-// TN GEMM for the SIREN weight gradient on gfx950 bf16 MFMA, split-K over coordinates.
+// TN GEMM for the SIREN weight gradient on gfx950 h16 MFMA, split-K over coordinates.
 //
 //   dW[o][k] = sum_n dZ[n][o] * Y[n][k]          (autograd addmm backward, models.py:114-115)
 //
@@ -48,11 +48,11 @@ __device__ __forceinline__ int tn_swz(int r) { return ((r & 3) | (((r >> 3) & 1)
 // [n][col] image (the second block sits 4 rows further down).
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 template <int ROW>
-__device__ __forceinline__ bf16x8 tr_frag(const char* p) {
+__device__ __forceinline__ h16x8 tr_frag(const char* p) {
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(p));
   const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(p + 4 * ROW));
   const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, v);
+  return __builtin_bit_cast(h16x8, v);
 }
 
 template <class Cfg>
@@ -93,8 +93,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
     const int ks = ks_begin + kt;
     char* ys = smem + buf * Cfg::STAGE + wave * Cfg::YINSTR * 1024;
     char* zs = smem + buf * Cfg::STAGE + Cfg::YBYTES + wave * Cfg::ZINSTR * 1024;
-    const bf16* yb = p.Y + (size_t)ks * BK * p.Hin;
-    const bf16* zb = p.dZ + (size_t)ks * BK * p.Hout;
+    const h16* yb = p.Y + (size_t)ks * BK * p.Hin;
+    const h16* zb = p.dZ + (size_t)ks * BK * p.Hout;
 #pragma unroll
     for (int j = 0; j < Cfg::YINSTR; ++j) glds16_asm(yb + yoff[j], lds_addr(ys + j * 1024));
 #pragma unroll
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
 #pragma unroll
     for (int j = 0; j < SJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto frags = [&](int slot, int kk, bf16x8 (&A)[SI], bf16x8 (&B)[SJ]) {
+  auto frags = [&](int slot, int kk, h16x8 (&A)[SI], h16x8 (&B)[SJ]) {
     const char* ys = smem + slot * Cfg::STAGE;
     const char* zs = ys + Cfg::YBYTES;
 #pragma unroll
@@ -182,8 +182,10 @@ hipError_t gemm_tn_dw(const TnParams& p, hipStream_t s) {
 //   k = ti*BI + wm*TI + i*16 + 4*(lane>>4) + {0..3},  o = tj*BJ + wn*TJ + j*16 + (lane&15)
 template <class Cfg>
 __global__ void dw_reduce_kernel(const float4* __restrict__ slab, int splits, int Hin, int Hout,
-                                 float* __restrict__ grad, int accumulate) {
+                                 float* __restrict__ grad, int accumulate,
+                                 const float* __restrict__ gscale) {
   constexpr int SUB = Cfg::SI * Cfg::SJ;
+  const float inv = gscale ? gscale[1] : 1.0f;  // undo the dZ storage scale (exact: 2^-k)
   const int tiles_j = Hout / Cfg::BJ;
   const int ntile = (Hin / Cfg::BI) * tiles_j;
   constexpr int TQ = Cfg::TILE_FLOATS / 4;
@@ -195,6 +197,7 @@ __global__ void dw_reduce_kernel(const float4* __restrict__ slab, int splits, in
       const float4 w = slab[q + s * total];
       v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
     }
+    v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
     const int tile = (int)(q / TQ);
     const int within = (int)(q - (int64_t)tile * TQ);
     const int lane = within & 63, blk = within >> 6;
@@ -216,16 +219,16 @@ __global__ void dw_reduce_kernel(const float4* __restrict__ slab, int splits, in
 }
 
 hipError_t dw_reduce(const float* slab, int splits, int Hin, int Hout, int tile, float* grad,
-                     int accumulate, hipStream_t s) {
+                     int accumulate, const float* gscale, hipStream_t s) {
   const int64_t total = (int64_t)Hin * Hout / 4;
   int grid = (int)((total + 255) / 256);
   if (grid > 4096) grid = 4096;
   if (tile == 256) {
     hipLaunchKernelGGL(dw_reduce_kernel<TnLarge>, dim3(grid), dim3(256), 0, s, (const float4*)slab, splits,
-                       Hin, Hout, grad, accumulate);
+                       Hin, Hout, grad, accumulate, gscale);
   } else if (tile == 128) {
     hipLaunchKernelGGL(dw_reduce_kernel<TnSmall>, dim3(grid), dim3(256), 0, s, (const float4*)slab, splits,
-                       Hin, Hout, grad, accumulate);
+                       Hin, Hout, grad, accumulate, gscale);
   } else {
     return hipErrorInvalidValue;
   }

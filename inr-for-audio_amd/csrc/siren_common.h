@@ -1,14 +1,14 @@
 // Shared device types and helpers for the SIREN gfx950 kernels.
 //
-// Everything here is CDNA4-only (wave64, bf16 MFMA, LDS-DMA); no portability layer.
+// Everything here is CDNA4-only (wave64, h16 MFMA, LDS-DMA); no portability layer.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-typedef __bf16 bf16;
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h16;
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -61,13 +61,13 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const LDS_AS char*)(p);
 }
 
-__device__ __forceinline__ bf16x4 pack4(float a, float b, float c, float d) {
-  bf16x4 r;
-  r[0] = (bf16)a; r[1] = (bf16)b; r[2] = (bf16)c; r[3] = (bf16)d;
+__device__ __forceinline__ h16x4 pack4(float a, float b, float c, float d) {
+  h16x4 r;
+  r[0] = (h16)a; r[1] = (h16)b; r[2] = (h16)c; r[3] = (h16)d;
   return r;
 }
 
-__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ float bf2f(h16 x) { return (float)x; }
 
 // 16x16 MFMA output layout -> 16-B row pieces.  A lane of 16-lane group g = lane>>4 holds 4
 // consecutive columns 4g..4g+3 (one row, lane&15) of two adjacent 16-column subtiles, a and b.
@@ -90,8 +90,8 @@ __device__ __forceinline__ void unswap16_pair(uint4 v, uint2& a, uint2& b) {
 // column offset (in elements, from the pair's first column) of this lane's 8-column piece
 __device__ __forceinline__ int swap16_col(int lane) { return ((lane >> 4) & 1) * 16 + 8 * (lane >> 5); }
 
-__device__ __forceinline__ uint2 as_u2(bf16x4 v) { return __builtin_bit_cast(uint2, v); }
-__device__ __forceinline__ bf16x4 as_bf4(uint2 v) { return __builtin_bit_cast(bf16x4, v); }
+__device__ __forceinline__ uint2 as_u2(h16x4 v) { return __builtin_bit_cast(uint2, v); }
+__device__ __forceinline__ h16x4 as_h4(uint2 v) { return __builtin_bit_cast(h16x4, v); }
 
 // Sum over the 16 lanes of a DPP row (lanes with equal lane>>4): fixed rotation order, result
 // in every lane of the row.
@@ -114,6 +114,18 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   float s = 0.f;
   for (int i = 0; i < nw; ++i) s += scratch[i];  // fixed order: deterministic
   return s;
+}
+
+// Block-wide max, same contract as block_sum.
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  float m = 0.f;
+  for (int i = 0; i < nw; ++i) m = fmaxf(m, scratch[i]);
+  return m;
 }
 
 }  // namespace siren

@@ -6,29 +6,31 @@
 
 namespace siren {
 
-typedef __bf16 bf16;
+typedef _Float16 h16;  // activation / weight-shadow / gradient storage (fp16)
 
 enum NtMode { NT_FWD = 0, NT_DX = 1, NT_DX0 = 2 };
 
 struct NtParams {
-  const bf16* X;  // [M][K]
-  const bf16* W;  // [N][K]
+  const h16* X;  // [M][K]
+  const h16* W;  // [N][K]
   int M, N, K;
   int tile;       // 128 or 256 (nt_choose_tile): partials are per tile-row / tile-column
   float omega;  // FWD: this layer's omega; DX: omega of the layer below; DX0: omega_0
   // NT_FWD
   const float* bias;    // [N]
-  bf16* Y;              // [M][N]
-  bf16* C;              // [M][N]
+  h16* Y;              // [M][N]
+  h16* C;              // [M][N]
   const float* head_w;  // [N]          (HEAD only)
   float* head_part;     // [N/128][M]   (HEAD only)
   // NT_DX / NT_DX0
-  const bf16* Cprev;    // [M][N]  cos of the layer below (NT_DX)
-  bf16* dZ;             // [M][N]  (NT_DX)
+  const h16* Cprev;    // [M][N]  cos of the layer below (NT_DX)
+  h16* dZ;             // [M][N]  (NT_DX)
   float* colsum_part;   // NT_DX: [M/128][N];  NT_DX0: [M/128][1+in][N]
   // NT_DX0 (Cprev = cos of the first layer)
   const float* t;       // [M][in]
   int in_dim;
+  const float* gscale;  // NT_DX / NT_DX0: {S, 1/S} -- column partials are multiplied by 1/S
+                        // (null = unscaled)
   int stagger;          // persistent grid: block b idles (b % 16) * stagger * ~1.7k cycles first
   unsigned long long* stamps;  // SIREN_NT_STAMPS diagnostic builds only
 };
@@ -42,8 +44,8 @@ void gemm_tn_set_pipe(int v);     // 256x256 K-loop variant (TnL0..TnL2)
 void gemm_nt_set_grid_cap(int cap);  // persistent grid size override (0 = #CUs)
 void gemm_nt_set_stagger(int units); // persistent grid start stagger (see NtParams::stagger)
 struct TnParams {
-  const bf16* Y;   // [R][Hin]   layer input (A role: dW column index k)
-  const bf16* dZ;  // [R][Hout]  layer pre-activation gradient (B role: dW row index o)
+  const h16* Y;   // [R][Hin]   layer input (A role: dW column index k)
+  const h16* dZ;  // [R][Hout]  layer pre-activation gradient (B role: dW row index o)
   int R, Hin, Hout;
   int splits;
   int tile;        // 128 or 256 (tn_choose_tile); dw_reduce must be given the same value
@@ -53,18 +55,24 @@ struct TnParams {
 int tn_choose_tile(int R, int Hin, int Hout);
 hipError_t gemm_tn_dw(const TnParams& p, hipStream_t s);
 // grad[o][k] (+)= sum_s slab[s]  (grad row-major [Hout][Hin])
+// (scaled by gscale[1] = 1/S when gscale is non-null: dZ carries the backward scale S)
 hipError_t dw_reduce(const float* slab, int splits, int Hin, int Hout, int tile, float* grad,
-                     int accumulate, hipStream_t s);
+                     int accumulate, const float* gscale, hipStream_t s);
 
 // elementwise / reduction kernels (elementwise.hip)
 hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, hipStream_t s);
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
-                     int R, int H, bf16* Y0, bf16* C0, hipStream_t s);
+                     int R, int H, h16* Y0, h16* C0, hipStream_t s);
 hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_head, const float* y,
-                     int n_valid, float gscale, float* out, float* g, float* sse_part,
-                     float* gsum_part, hipStream_t s);
-hipError_t head_bwd(const bf16* C, const bf16* Y, const float* g, const float* w_head, float omega,
-                    int R, int H, bf16* dZ, float* db_part, float* dwh_part, hipStream_t s);
+                     int n_valid, float gfac, float* out, float* g, float* sse_part,
+                     float* gsum_part, float* gmax_part, hipStream_t s);
+hipError_t gmax_partials(const float* g, int R, float* gmax_part, hipStream_t s);
+// gscale[0] = S (dZ storage scale), gscale[1] = 1/S; from (R+255)/256 max|g| partials
+hipError_t grad_scale(const float* gmax_part, int nparts, const float* w_head, int H, float omega,
+                      float* gscale, hipStream_t s);
+hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_head, float omega,
+                    int R, int H, const float* gscale, h16* dZ, float* db_part, float* dwh_part,
+                    hipStream_t s);
 // out[c*out_stride] (+)= sum_r part[r*row_stride + c]; tmp holds >= 64*ncols floats
 hipError_t col_reduce(const float* part, int64_t row_stride, int nrows, int ncols, float* out,
                       int out_stride, int accumulate, float* tmp, hipStream_t s);
@@ -84,7 +92,7 @@ hipError_t adam_flat(float* p, const float* g, float* m, float* v, int64_t n, co
                      hipStream_t s);
 hipError_t plateau_step(OptState* st, const float* sse, double n_total, float* loss_hist,
                         double* lr_hist, int64_t hist_cap, hipStream_t s);
-hipError_t cast_weight(const float* W, int H_out, int H_in, bf16* Wb, bf16* WTb, hipStream_t s);
+hipError_t cast_weight(const float* W, int H_out, int H_in, h16* Wb, h16* WTb, hipStream_t s);
 hipError_t sum_to(const float* x, int n, float* out, int accumulate, hipStream_t s);
 
 }  // namespace siren

@@ -6,9 +6,10 @@ forward, MSELoss, backward, Adam, ReduceLROnPlateau.  The engine owns
 * a flat fp32 parameter vector (plus grad / exp_avg / exp_avg_sq vectors of the same
   layout) whose segments the nn.Module parameters are re-pointed at, so
   ``model.state_dict()`` always shows the live weights;
-* bf16 shadows W_i and W_i^T of every hidden weight (refreshed by the update kernel);
-* one micro-batch workspace (bf16 activations Y_i = sin, C_i = cos, dZ ping-pong and fp32
-  partial-sum slabs), reused for every micro-batch of the full-batch step;
+* fp16 shadows W_i and W_i^T of every hidden weight (refreshed by the update kernel);
+* one micro-batch workspace (fp16 activations Y_i = sin, C_i = cos, scaled fp16 dZ
+  ping-pong and fp32 partial-sum slabs), reused for every micro-batch of the full-batch
+  step -- fp16, not bf16: DESIGN.md "Storage precision";
 * the optimizer / scheduler state as a device struct, so a step needs no host sync and
   can be captured in a HIP graph.
 
@@ -28,6 +29,7 @@ from . import _lib
 from ._lib import MAX_INNER, ROW_TILE, SirenBatch, SirenGrads, SirenNet, SirenOptState, check, ptr
 
 SEG_ALIGN = 64  # floats: every flat segment starts 256-B aligned
+STORE16 = torch.float16  # activation / weight-shadow / dZ storage of the HIP path
 
 
 def round_up(x: int, m: int) -> int:
@@ -81,21 +83,23 @@ class Workspace:
         if rows % ROW_TILE:
             raise ValueError(f"rows={rows} must be a multiple of {ROW_TILE}")
         H, L, R = spec.hidden, spec.n_inner, rows
-        bf, f32 = torch.bfloat16, torch.float32
+        h, f32 = STORE16, torch.float32
         e = lambda *s, dtype=f32: torch.empty(*s, dtype=dtype, device=device)  # noqa: E731
         self.rows = R
-        self.Y = [e(R, H, dtype=bf) for _ in range(L + 1)]
-        self.C = [e(R, H, dtype=bf) for _ in range(L + 1)]
+        self.Y = [e(R, H, dtype=h) for _ in range(L + 1)]
+        self.C = [e(R, H, dtype=h) for _ in range(L + 1)]
         self.out = e(R)
         self.g = torch.zeros(R, dtype=f32, device=device)
         self.head_part = e(H // 128, R)
         nsum = (R + 255) // 256
         self.sse_part = e(nsum)
         self.gsum_part = e(nsum)
+        self.gmax_part = e(nsum)
+        self.gscale = torch.ones(2, dtype=f32, device=device)
         self.train = train
         if train:
             self.splits = int(splits or lib.siren_default_splits(R, H))
-            self.dZ = [e(R, H, dtype=bf) for _ in range(2)]
+            self.dZ = [e(R, H, dtype=h) for _ in range(2)]
             self.col_part = e(R // 128, 1 + spec.in_dim, H)
             self.col_part2 = e(R // 128, H)
             self.red_tmp = e(64, H)
@@ -118,18 +122,19 @@ class Workspace:
         b.dZ[0], b.dZ[1] = ptr(self.dZ[0]), ptr(self.dZ[1])
         b.out, b.g, b.head_part = ptr(self.out), ptr(self.g), ptr(self.head_part)
         b.sse_part, b.gsum_part = ptr(self.sse_part), ptr(self.gsum_part)
+        b.gmax_part, b.gscale = ptr(self.gmax_part), ptr(self.gscale)
         b.col_part, b.col_part2 = ptr(self.col_part), ptr(self.col_part2)
         b.red_tmp, b.slab = ptr(self.red_tmp), ptr(self.slab)
         return b
 
 
-def make_net(spec: NetSpec, W0, b0, bs, Wbs, WTbs, w_head, b_head) -> SirenNet:
+def make_net(spec: NetSpec, W0, b0, bs, Whs, WThs, w_head, b_head) -> SirenNet:
     n = SirenNet()
     n.in_dim, n.hidden, n.n_inner = spec.in_dim, spec.hidden, spec.n_inner
     n.omega0, n.omega = spec.omega0, spec.omega
     n.W0, n.b0 = ptr(W0), ptr(b0)
     for i in range(spec.n_inner):
-        n.b[i], n.Wb[i], n.WTb[i] = ptr(bs[i]), ptr(Wbs[i]), ptr(WTbs[i])
+        n.b[i], n.Wh[i], n.WTh[i] = ptr(bs[i]), ptr(Whs[i]), ptr(WThs[i])
     n.w_head, n.b_head = ptr(w_head), ptr(b_head)
     return n
 
@@ -147,10 +152,10 @@ def make_grads(spec: NetSpec, layout: ParamLayout, gflat: torch.Tensor) -> Siren
     return g
 
 
-def cast_shadows(spec, Ws, Wbs, WTbs, stream):
+def cast_shadows(spec, Ws, Whs, WThs, stream):
     lib = _lib.load()
-    for W, Wb, WTb in zip(Ws, Wbs, WTbs):
-        check(lib.siren_cast_weight(ptr(W), spec.hidden, spec.hidden, ptr(Wb), ptr(WTb), stream),
+    for W, Wh, WTh in zip(Ws, Whs, WThs):
+        check(lib.siren_cast_weight(ptr(W), spec.hidden, spec.hidden, ptr(Wh), ptr(WTh), stream),
               "siren_cast_weight")
 
 
@@ -200,14 +205,14 @@ class SirenEngine:
         L, H = spec.n_inner, spec.hidden
         pv = lambda i: lay.view(self.params, i)  # noqa: E731
         self.W = [pv(2 + 2 * i) for i in range(L)]
-        self.Wb = [torch.empty(H, H, dtype=torch.bfloat16, device=dev) for _ in range(L)]
-        self.WTb = [torch.empty(H, H, dtype=torch.bfloat16, device=dev) for _ in range(L)]
-        self.net = make_net(spec, pv(0), pv(1), [pv(3 + 2 * i) for i in range(L)], self.Wb, self.WTb,
+        self.Wh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
+        self.WTh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
+        self.net = make_net(spec, pv(0), pv(1), [pv(3 + 2 * i) for i in range(L)], self.Wh, self.WTh,
                             pv(2 + 2 * L), pv(3 + 2 * L))
         self.grad_struct = make_grads(spec, lay, self.grads)
         self._Wp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.W])
-        self._Wbp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.Wb])
-        self._WTbp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.WTb])
+        self._Whp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.Wh])
+        self._WThp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.WTh])
 
         # optimizer + scheduler state (torch defaults of run.py:116-117)
         st = SirenOptState()
@@ -255,7 +260,7 @@ class SirenEngine:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def _refresh_shadows(self):
-        cast_shadows(self.spec, self.W, self.Wb, self.WTb, self._stream())
+        cast_shadows(self.spec, self.W, self.Wh, self.WTh, self._stream())
 
     def _launch_grads(self):
         s = self._stream()
@@ -266,7 +271,7 @@ class SirenEngine:
     def _launch_update(self):
         check(self.lib.siren_apply_update(
             ctypes.byref(self.net), ptr(self.params), ptr(self.grads), ptr(self.exp_avg),
-            ptr(self.exp_avg_sq), self.layout.n_params, self._Wp, self._Wbp, self._WTbp,
+            ptr(self.exp_avg_sq), self.layout.n_params, self._Wp, self._Whp, self._WThp,
             ptr(self.state), self.grads.data_ptr() + 4 * self.layout.sse_offset, float(self.n_total),
             ptr(self.loss_hist), ptr(self.lr_hist), self.hist_cap, self._stream()),
             "siren_apply_update")

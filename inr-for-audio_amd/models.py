@@ -143,7 +143,7 @@ class _SirenFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, spec, coords, *params):
-        from .engine import ROW_TILE, Workspace, cast_shadows, make_net, round_up
+        from .engine import ROW_TILE, STORE16, Workspace, cast_shadows, make_net, round_up
         dev = coords.device
         lib = _lib.load()
         L, H = spec.n_inner, spec.hidden
@@ -151,11 +151,11 @@ class _SirenFunction(torch.autograd.Function):
         rows = round_up(max(n, 1), ROW_TILE)
         p = [t.detach().contiguous().float() for t in params]
         W = [p[2 + 2 * i] for i in range(L)]
-        Wb = [torch.empty(H, H, dtype=torch.bfloat16, device=dev) for _ in range(L)]
-        WTb = [torch.empty(H, H, dtype=torch.bfloat16, device=dev) for _ in range(L)]
+        Wh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
+        WTh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
         s = torch.cuda.current_stream(dev).cuda_stream
-        cast_shadows(spec, W, Wb, WTb, s)
-        net = make_net(spec, p[0], p[1], [p[3 + 2 * i] for i in range(L)], Wb, WTb, p[2 + 2 * L],
+        cast_shadows(spec, W, Wh, WTh, s)
+        net = make_net(spec, p[0], p[1], [p[3 + 2 * i] for i in range(L)], Wh, WTh, p[2 + 2 * L],
                        p[3 + 2 * L])
         ws = Workspace(spec, rows, dev, train=True)
         xc = torch.zeros(rows, spec.in_dim, dtype=torch.float32, device=dev)
@@ -163,14 +163,14 @@ class _SirenFunction(torch.autograd.Function):
         tgt = torch.zeros(rows, dtype=torch.float32, device=dev)
         b = ws.batch(xc, tgt, n, float(n))
         _lib.check(lib.siren_forward(ctypes.byref(net), ctypes.byref(b), s), "siren_forward")
-        ctx.keep = (spec, net, ws, xc, tgt, p, Wb, WTb, n, [t.shape for t in params])
+        ctx.keep = (spec, net, ws, xc, tgt, p, Wh, WTh, n, [t.shape for t in params])
         return ws.out[:n].clone()
 
     @staticmethod
     def backward(ctx, grad_out):
         from .engine import SEG_ALIGN, round_up
         from ._lib import SirenGrads, ptr
-        spec, net, ws, xc, tgt, p, Wb, WTb, n, shapes = ctx.keep
+        spec, net, ws, xc, tgt, p, Wh, WTh, n, shapes = ctx.keep
         lib = _lib.load()
         dev = xc.device
         L = spec.n_inner

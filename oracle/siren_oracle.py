@@ -17,9 +17,11 @@ Pinned against golden vectors generated from the reference itself (tests/golden/
 made by tests/golden/make_golden.py, which imports /root/reference in the build
 container); see tests/test_oracle.py.
 
-Precision model: `dtype=np.float64` gives the exact-arithmetic answer; `bf16=True`
-rounds exactly the tensors the HIP path stores in bf16 (hidden weights, Y_i = sin,
-C_i = cos, dZ_i) so the GPU can be checked tightly against it.
+Precision model: `dtype=np.float64` gives the exact-arithmetic answer; `half=True`
+rounds exactly the tensors the HIP path stores in fp16 (hidden weights, Y_i = sin,
+C_i = cos, and dZ_i multiplied by the power-of-two backward scale S of grad_scale()) so
+the GPU can be checked tightly against it.  `bf16_round` is kept for the precision study
+(tools/fit_torch_diag.py, DESIGN.md "Storage precision").
 """
 from __future__ import annotations
 
@@ -42,6 +44,22 @@ def bf16_round(x: np.ndarray) -> np.ndarray:
     nan = np.isnan(x)
     out[nan] = x[nan]
     return out
+
+
+def f16_round(x: np.ndarray) -> np.ndarray:
+    """Round-to-nearest-even to IEEE fp16 (v_cvt_f16_f32 semantics), returned as float32."""
+    return np.asarray(x, F32).astype(np.float16).astype(F32)
+
+
+def grad_scale(g: np.ndarray, wf: np.ndarray, omega: float) -> float:
+    """elementwise.hip grad_scale_kernel: S = 2^(6-e) with max|g|*max|w_head|*|omega| in
+    [2^(e-1), 2^e) (fp32 product), k clamped to [-100, 100]; S = 1 if the bound is 0."""
+    bound = F32(F32(np.max(np.abs(np.asarray(g, F32)))) * F32(np.max(np.abs(np.asarray(wf, F32)))))
+    bound = F32(bound * F32(abs(omega)))
+    if not (bound > 0 and np.isfinite(bound)):
+        return 1.0
+    _, e = math.frexp(float(bound))
+    return math.ldexp(1.0, int(min(max(6 - e, -100), 100)))
 
 
 def fma32(a, b, c) -> np.ndarray:
@@ -128,25 +146,25 @@ def cos32(a: np.ndarray) -> np.ndarray:
     return np.cos(np.asarray(a, F64)).astype(F32)
 
 
-def forward(p: Params, t: np.ndarray, omega0: float, omega: float, bf16: bool = False,
+def forward(p: Params, t: np.ndarray, omega0: float, omega: float, half: bool = False,
             dtype=F32):
     """Returns (out [N], cache).  cache: Y[0..L] (layer outputs), A[0..L] (omega*linear),
-    C[1..L] cos of inner pre-activations; bf16-rounded where the HIP path stores bf16."""
+    C[0..L] cos of the pre-activations; fp16-rounded where the HIP path stores fp16."""
     A0 = first_preact(t, p.W0, p.b0, omega0)
     Y0 = sin32(A0)
-    Y = [bf16_round(Y0) if bf16 else Y0]
+    Y = [f16_round(Y0) if half else Y0]
     C0 = cos32(A0)
-    A, C = [A0], [bf16_round(C0) if bf16 else C0]
+    A, C = [A0], [f16_round(C0) if half else C0]
     for Wi, bi in zip(p.W, p.b):
-        Wm = bf16_round(Wi) if bf16 else Wi
+        Wm = f16_round(Wi) if half else Wi
         z = np.asarray(Y[-1], dtype) @ np.asarray(Wm, dtype).T + np.asarray(bi, dtype)
         a = (F64(omega) * np.asarray(z, F64)) if dtype == F64 else (F32(omega) * z.astype(F32))
         y, c = np.sin(a), np.cos(a)
-        if bf16:
-            y, c = bf16_round(y), bf16_round(c)
+        if half:
+            y, c = f16_round(y), f16_round(c)
         A.append(a)
-        Y.append(np.asarray(y, dtype if not bf16 else F32))
-        C.append(np.asarray(c, dtype if not bf16 else F32))
+        Y.append(np.asarray(y, dtype if not half else F32))
+        C.append(np.asarray(c, dtype if not half else F32))
     out = np.asarray(Y[-1], dtype) @ np.asarray(p.wf, dtype) + dtype(p.bf)
     return out, {"Y": Y, "A": A, "C": C}
 
@@ -157,29 +175,29 @@ def mse(out: np.ndarray, y: np.ndarray) -> float:
 
 
 def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float, omega: float,
-             bf16: bool = False, dtype=F64) -> dict:
+             half: bool = False, dtype=F64) -> dict:
     """Autograd of the SIREN for upstream dLoss/dout = g [N].  Returns a dict of grads in
-    nn.Linear layout (same keys as Params.to_state_dict)."""
+    nn.Linear layout (same keys as Params.to_state_dict).  With `half`, every dZ_i is
+    rounded as the HIP path stores it: fp16(dZ_i * S) / S (exact power-of-two scale)."""
     L = len(p.W)
     Y, A, C = cache["Y"], cache["A"], cache["C"]
+    S = grad_scale(g, p.wf, omega) if half else 1.0
     g = np.asarray(g, dtype).reshape(-1)
     grads = {}
     grads[f"net.{L + 1}.weight"] = (g @ np.asarray(Y[L], dtype)).reshape(1, -1)
     grads[f"net.{L + 1}.bias"] = np.array([g.sum()])
     dY = g[:, None] * np.asarray(p.wf, dtype)[None, :]
     for i in range(L, 0, -1):
-        cos_i = np.asarray(C[i], dtype) if bf16 else np.cos(np.asarray(A[i], F64)).astype(dtype)
+        cos_i = np.asarray(C[i], dtype) if half else np.cos(np.asarray(A[i], F64)).astype(dtype)
         dZ = dY * cos_i * dtype(omega)
-        if bf16:
-            db = dZ.sum(0)
-            dZ = bf16_round(dZ).astype(dtype)
-        else:
-            db = dZ.sum(0)
+        db = dZ.sum(0)
+        if half:
+            dZ = (np.asarray(dZ * S, F32).astype(np.float16).astype(dtype) / S).astype(dtype)
         grads[f"net.{i}.linear.weight"] = dZ.T @ np.asarray(Y[i - 1], dtype)
         grads[f"net.{i}.linear.bias"] = db
-        Wm = bf16_round(p.W[i - 1]) if bf16 else p.W[i - 1]
+        Wm = f16_round(p.W[i - 1]) if half else p.W[i - 1]
         dY = dZ @ np.asarray(Wm, dtype)
-    cos0 = np.asarray(C[0], dtype) if bf16 else np.cos(np.asarray(A[0], F64)).astype(dtype)
+    cos0 = np.asarray(C[0], dtype) if half else np.cos(np.asarray(A[0], F64)).astype(dtype)
     dZ0 = dY * cos0 * dtype(omega0)
     tt = np.asarray(t, dtype).reshape(dZ0.shape[0], -1)
     grads["net.0.linear.weight"] = dZ0.T @ tt
@@ -249,7 +267,7 @@ def reported_snr(ref_raw, fs, rec, duration, decimation=1) -> float:
 
 
 # ------------------------------------------------------------------ full-batch fit (run.py:156-190)
-def fit(p: Params, t, y, omega0, omega, steps, lr=1e-3, min_lr=1e-6, bf16=False):
+def fit(p: Params, t, y, omega0, omega, steps, lr=1e-3, min_lr=1e-6, half=False):
     """Full-batch fit with the restated loop; returns (params, losses, lrs)."""
     names = list(p.to_state_dict().keys())
     flat = [x.astype(F32).copy() for x in p.to_state_dict().values()]
@@ -260,9 +278,9 @@ def fit(p: Params, t, y, omega0, omega, steps, lr=1e-3, min_lr=1e-6, bf16=False)
     L = len(p.W)
     for k in range(1, steps + 1):
         cur = Params.from_state_dict(dict(zip(names, flat)), L)
-        out, cache = forward(cur, t, omega0, omega, bf16=bf16)
+        out, cache = forward(cur, t, omega0, omega, half=half)
         loss = F32(mse(out, y))
-        grads = backward(cur, t, cache, mse_grad(out, y), omega0, omega, bf16=bf16)
+        grads = backward(cur, t, cache, mse_grad(out, y), omega0, omega, half=half)
         for j, nme in enumerate(names):
             flat[j], ms[j], vs[j] = adam_step(flat[j], grads[nme].astype(F32).reshape(flat[j].shape),
                                               ms[j], vs[j], k, sched.lr)

@@ -35,7 +35,7 @@ def test_binding_table_matches_header(lib):
 
 
 def test_host_only_helpers(lib):
-    assert lib.siren_abi_version() == 1
+    assert lib.siren_abi_version() == 2
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256
@@ -58,7 +58,9 @@ def test_validation_without_device(lib):
                                None) == 1002
     assert lib.siren_inner_bwd_dw(1, 1, 100, 256, 1, 0, 1, None) == 1001  # rows % 64
     assert lib.siren_inner_bwd_dw(1, 1, 128, 256, 1, 64, 1, None) == 1003  # bad tile
-    assert lib.siren_dw_reduce(1, 1, 256, 0, 1, 1, None) == 1003           # tile must be explicit
+    assert lib.siren_dw_reduce(1, 1, 256, 0, 1, 1, None, None) == 1003     # tile must be explicit
+    assert lib.siren_grad_scale(None, 1, 1, 256, ctypes.c_float(30), 1, None) == 1002
+    assert lib.siren_grad_scale(1, 0, 1, 256, ctypes.c_float(30), 1, None) == 1001
     assert lib.siren_first_fwd(1, 3, 1, 1, ctypes.c_float(1.0), 128, 256, 1, 1, None) == 1003
 
 
@@ -66,4 +68,4 @@ def test_validation_without_device(lib):
 def test_supported_hidden_sizes_validate(lib, hidden):
     # only shape checks run (NULL outputs make it return before any launch)
     assert lib.siren_head_bwd(None, None, None, None, ctypes.c_float(30), 128, hidden, None, None, None,
-                              None) == 1002
+                              None, None) == 1002

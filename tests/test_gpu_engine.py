@@ -48,11 +48,11 @@ def test_train_step_grads_vs_oracle(dev, H, L, n, w0, in_dim, mb):
     torch.cuda.synchronize()
     got = {k: v.detach().cpu().numpy() for k, v in zip(eng.layout.names, eng.grad_views())}
     p = orc.Params.from_state_dict(sd0, L)
-    out, cache = orc.forward(p, t.numpy(), w0, 30.0, bf16=True, dtype=np.float64)
-    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), w0, 30.0, bf16=True)
+    out, cache = orc.forward(p, t.numpy(), w0, 30.0, half=True, dtype=np.float64)
+    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), w0, 30.0, half=True)
     for k, r in ref.items():
         assert _rel(got[k].reshape(r.shape), r) < 2e-2, k
-    # loss of step 0 and the fp32 (no-bf16) oracle loss agree to bf16 accuracy
+    # loss of step 0 and the fp32 (no-fp16-storage) oracle loss agree to storage accuracy
     out32, _ = orc.forward(p, t.numpy(), w0, 30.0)
     assert abs(eng.last_loss() - orc.mse(out32, y.numpy())) < 2e-2 * orc.mse(out32, y.numpy())
     # Adam applied with the device gradients is bit-exact with the oracle Adam on them
@@ -84,8 +84,8 @@ def test_train_step_forced_tiles(lib, dev, tile):
         lib.siren_set_option(4, 0)
     got = {k: v.detach().cpu().numpy() for k, v in zip(eng.layout.names, eng.grad_views())}
     p = orc.Params.from_state_dict(sd0, L)
-    out, cache = orc.forward(p, t.numpy(), w0, 30.0, bf16=True, dtype=np.float64)
-    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), w0, 30.0, bf16=True)
+    out, cache = orc.forward(p, t.numpy(), w0, 30.0, half=True, dtype=np.float64)
+    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), w0, 30.0, half=True)
     for k, r in ref.items():
         assert _rel(got[k].reshape(r.shape), r) < 2e-2, k
 
@@ -142,9 +142,9 @@ def test_forward_and_autograd_vs_oracle(dev):
     loss = torch.nn.functional.mse_loss(out, y.reshape(1, -1, 1).to(dev))
     loss.backward()
     p = orc.Params.from_state_dict(sd0, L)
-    o_ref, cache = orc.forward(p, t.numpy(), w0, 30.0, bf16=True, dtype=np.float64)
+    o_ref, cache = orc.forward(p, t.numpy(), w0, 30.0, half=True, dtype=np.float64)
     assert _rel(out.detach().cpu().numpy().reshape(-1), o_ref) < 1e-2
-    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(o_ref, y.numpy()), w0, 30.0, bf16=True)
+    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(o_ref, y.numpy()), w0, 30.0, half=True)
     for (k, prm) in model.named_parameters():
         assert _rel(prm.grad.cpu().numpy().reshape(ref[k].shape), ref[k]) < 3e-2, k
 

@@ -1,9 +1,10 @@
 """Per-kernel parity of libsiren_hip.so against the CPU oracle (called through the C-ABI).
 
-Tolerances: bf16-stored outputs (Y = sin, C = cos, dZ) must be within one bf16 rounding of
-the fp64 answer computed from the same bf16 inputs (|err| <= 2^-8 |x| + small fp32
-accumulation slack); fp32 reductions within 1e-5 relative; Adam and the coordinate grid
-bit-exact.
+Tolerances: fp16-stored outputs (Y = sin, C = cos, dZ) must be within one fp16 rounding of
+the fp64 answer computed from the same fp16 inputs (|err| <= 2^-11 |x| + small fp32
+accumulation slack); fp32 reductions within 1e-5 relative; Adam, the coordinate grid, the
+weight shadows and the backward scale bit-exact.  The backward storage scale S (gscale =
+{S, 1/S}) is exercised both as NULL (S = 1) and as a non-trivial power of two.
 """
 import ctypes
 import math
@@ -76,15 +77,24 @@ def _skip_tile(tile, R, H):
         pytest.skip("256-tile needs rows and hidden multiples of 256")
 
 
-def bf16_np(t: torch.Tensor) -> np.ndarray:
+H16 = torch.float16
+
+
+def f16_np(t: torch.Tensor) -> np.ndarray:
     return t.float().cpu().numpy()
 
 
-def within_bf16(got, ref, abs_slack=1e-5):
-    """|got - ref| <= 2^-8 * |ref| + abs_slack elementwise (one bf16 rounding + slack)."""
+def within_f16(got, ref, abs_slack=1e-5):
+    """|got - ref| <= 2^-11 * |ref| + abs_slack elementwise (one fp16 rounding + slack;
+    2^-25 covers the subnormal spacing)."""
     err = np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64))
-    bound = np.abs(np.asarray(ref, np.float64)) * 2.0 ** -8 + abs_slack
+    bound = np.abs(np.asarray(ref, np.float64)) * 2.0 ** -11 + abs_slack + 2.0 ** -25
     return float(np.max(err - bound))
+
+
+def gscale_dev(dev, k):
+    """{S, 1/S} with S = 2^k, or None (NULL: unscaled)."""
+    return None if k is None else to_dev(np.array([2.0 ** k, 2.0 ** -k], F32), dev)
 
 
 @pytest.mark.parametrize("n,rows,offset", [(1, 128, 0), (7, 128, 0), (44100, 44160, 0),
@@ -108,18 +118,18 @@ def test_first_fwd(lib, dev, in_dim, omega0):
     t = rng.uniform(-1, 1, (R, in_dim)).astype(F32)
     W0 = rng.uniform(-1, 1, (H, in_dim)).astype(F32)
     b0 = rng.uniform(-1, 1, H).astype(F32)
-    Y0 = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    Y0 = torch.empty(R, H, dtype=H16, device=dev)
     C0 = torch.empty_like(Y0)
     ok(lib.siren_first_fwd(ptr(to_dev(t, dev)), in_dim, ptr(to_dev(W0, dev)), ptr(to_dev(b0, dev)),
                            ctypes.c_float(omega0), R, H, ptr(Y0), ptr(C0), S()), lib)
     a0 = orc.first_preact(t, W0, b0, omega0)  # fp32 restatement (torch addmm rounding)
-    for got, ref in ((bf16_np(Y0), orc.sin32(a0)), (bf16_np(C0), orc.cos32(a0))):
-        assert within_bf16(got, ref, abs_slack=1e-6) <= 0
-        assert np.mean(got == orc.bf16_round(ref)) > 0.995
+    for got, ref in ((f16_np(Y0), orc.sin32(a0)), (f16_np(C0), orc.cos32(a0))):
+        assert within_f16(got, ref, abs_slack=1e-6) <= 0
+        assert np.mean(got == orc.f16_round(ref)) > 0.995
 
 
 def _inner_inputs(rng, R, H):
-    X = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    X = orc.f16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
     lim = math.sqrt(6 / H) / 30
     W = rng.uniform(-lim, lim, (H, H)).astype(F32)
     b = rng.uniform(-1 / math.sqrt(H), 1 / math.sqrt(H), H).astype(F32)
@@ -132,17 +142,17 @@ def test_inner_fwd(lib, dev, R, H, head, nt_tile):
     _skip_tile(nt_tile, R, H)
     rng = np.random.default_rng(2)
     X, W, b = _inner_inputs(rng, R, H)
-    Wb = orc.bf16_round(W)
+    Wh = orc.f16_round(W)
     hw = rng.uniform(-0.01, 0.01, H).astype(F32)
-    Y = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    Y = torch.empty(R, H, dtype=H16, device=dev)
     C = torch.empty_like(Y)
     hp = torch.zeros(H // 128, R, device=dev)
-    ok(lib.siren_inner_fwd(ptr(to_dev(X, dev, torch.bfloat16)), ptr(to_dev(Wb, dev, torch.bfloat16)),
+    ok(lib.siren_inner_fwd(ptr(to_dev(X, dev, H16)), ptr(to_dev(Wh, dev, H16)),
                            ptr(to_dev(b, dev)), ctypes.c_float(30.0), R, H, ptr(Y), ptr(C),
                            ptr(to_dev(hw, dev)) if head else None, ptr(hp) if head else None, S()), lib)
-    a = 30.0 * (X.astype(np.float64) @ Wb.astype(np.float64).T + b)
-    assert within_bf16(bf16_np(Y), np.sin(a), 2e-5) <= 0
-    assert within_bf16(bf16_np(C), np.cos(a), 2e-5) <= 0
+    a = 30.0 * (X.astype(np.float64) @ Wh.astype(np.float64).T + b)
+    assert within_f16(f16_np(Y), np.sin(a), 2e-5) <= 0
+    assert within_f16(f16_np(C), np.cos(a), 2e-5) <= 0
     if head:
         ref = np.sin(a) @ hw.astype(np.float64)
         got = hp.cpu().numpy().astype(np.float64).sum(0)
@@ -159,8 +169,10 @@ def test_head_loss(lib, dev):
     g = torch.empty(R, device=dev)
     sse = torch.empty((R + 255) // 256, device=dev)
     gs = torch.empty_like(sse)
+    gm = torch.empty_like(sse)
     ok(lib.siren_head_loss(ptr(to_dev(hp, dev)), nparts, R, ptr(to_dev(bh, dev)), ptr(to_dev(y, dev)),
-                           n_valid, ctypes.c_double(n_total), ptr(out), ptr(g), ptr(sse), ptr(gs), S()),
+                           n_valid, ctypes.c_double(n_total), ptr(out), ptr(g), ptr(sse), ptr(gs),
+                           ptr(gm), S()),
        lib)
     o_ref = hp.astype(np.float64).sum(0) + 0.25
     assert np.allclose(out.cpu().numpy(), o_ref, atol=1e-5)
@@ -168,47 +180,76 @@ def test_head_loss(lib, dev):
     assert np.allclose(g.cpu().numpy(), g_ref, rtol=1e-5, atol=1e-9)
     assert abs(sse.cpu().numpy().astype(np.float64).sum() - np.sum((o_ref - y)[:n_valid] ** 2)) < 1e-3
     assert abs(gs.cpu().numpy().astype(np.float64).sum() - g_ref.sum()) < 1e-6
+    g_dev = g.cpu().numpy()
+    assert np.array_equal(gm.cpu().numpy(), np.abs(g_dev).reshape(-1, 256).max(1))
+
+
+@pytest.mark.parametrize("gmag,wmag,omega", [(1e-3, 0.01, 30.0), (3e-10, 0.2, 30.0), (0.0, 0.1, 30.0),
+                                             (5e-6, 1e-30, 3000.0), (1.0, 1.0, 1.0)])
+def test_grad_scale_bit_exact(lib, dev, gmag, wmag, omega):
+    rng = np.random.default_rng(12)
+    R, H = 4096, 512
+    g = (rng.normal(size=R) * gmag).astype(F32)
+    w = (rng.uniform(-1, 1, H) * wmag).astype(F32)
+    part = np.abs(g).reshape(-1, 256).max(1).astype(F32)
+    out = torch.zeros(2, device=dev)
+    ok(lib.siren_grad_scale(ptr(to_dev(part, dev)), part.size, ptr(to_dev(w, dev)), H,
+                            ctypes.c_float(omega), ptr(out), S()), lib)
+    s_ref = orc.grad_scale(g, w, omega)
+    got = out.cpu().numpy()
+    assert got[0] == np.float32(s_ref) and got[1] == np.float32(1.0 / s_ref)
+    bound = float(np.max(np.abs(g))) * float(np.max(np.abs(w))) * omega
+    if bound > 0:
+        assert 2.0 ** 5 <= bound * s_ref < 2.0 ** 6 or s_ref in (2.0 ** 100, 2.0 ** -100)
 
 
 @pytest.mark.parametrize("H", [128, 256, 1024])
-def test_head_bwd(lib, dev, H):
+@pytest.mark.parametrize("gmag,k", [(1e-3, None), (1e-9, 27)])
+def test_head_bwd(lib, dev, H, gmag, k):
+    """dZ is stored x S (k = log2 S; 1e-9 gradients would underflow fp16 unscaled); the db /
+    dw_head partials stay unscaled."""
     rng = np.random.default_rng(4)
     R = 512
-    C = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
-    Y = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
-    g = rng.normal(size=R).astype(F32) * 1e-3
+    C = orc.f16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    Y = orc.f16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    g = rng.normal(size=R).astype(F32) * gmag
     w = rng.uniform(-0.01, 0.01, H).astype(F32)
-    dZ = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    dZ = torch.empty(R, H, dtype=H16, device=dev)
     dbp = torch.empty(R // 128, H, device=dev)
     dwp = torch.empty(R // 128, H, device=dev)
-    ok(lib.siren_head_bwd(ptr(to_dev(C, dev, torch.bfloat16)), ptr(to_dev(Y, dev, torch.bfloat16)),
-                          ptr(to_dev(g, dev)), ptr(to_dev(w, dev)), ctypes.c_float(30.0), R, H, ptr(dZ),
-                          ptr(dbp), ptr(dwp), S()), lib)
+    ok(lib.siren_head_bwd(ptr(to_dev(C, dev, H16)), ptr(to_dev(Y, dev, H16)),
+                          ptr(to_dev(g, dev)), ptr(to_dev(w, dev)), ctypes.c_float(30.0), R, H,
+                          ptr(gscale_dev(dev, k)), ptr(dZ), ptr(dbp), ptr(dwp), S()), lib)
+    sc = 2.0 ** (k or 0)
     dz_ref = g[:, None].astype(np.float64) * w[None, :] * C * 30.0
-    assert within_bf16(bf16_np(dZ), dz_ref, 1e-12) <= 0
-    assert np.allclose(dbp.cpu().numpy().astype(np.float64).sum(0), dz_ref.sum(0), rtol=1e-4, atol=1e-9)
-    assert np.allclose(dwp.cpu().numpy().astype(np.float64).sum(0), (g[:, None] * Y).sum(0), rtol=1e-4,
-                       atol=1e-9)
+    assert within_f16(f16_np(dZ), dz_ref * sc, 1e-12) <= 0
+    # fp32 partial sums vs fp64, tolerance relative to the sum of |terms| (cancellation)
+    gy = g[:, None].astype(np.float64) * Y
+    for got, terms in ((dbp, dz_ref), (dwp, gy)):
+        err = np.abs(got.cpu().numpy().astype(np.float64).sum(0) - terms.sum(0))
+        assert np.all(err <= 1e-5 * np.abs(terms).sum(0) + 1e-12)
 
 
 @pytest.mark.parametrize("R,H", [(256, 128), (512, 256), (256, 1024), (768, 512)])
-def test_inner_bwd_dx(lib, dev, R, H, nt_tile):
+@pytest.mark.parametrize("k", [None, 9])
+def test_inner_bwd_dx(lib, dev, R, H, k, nt_tile):
+    """dZprev carries the input's scale; the db partials come out x 1/S."""
     _skip_tile(nt_tile, R, H)
     rng = np.random.default_rng(5)
-    dZ = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
+    dZ = orc.f16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
     _, W, _ = _inner_inputs(rng, R, H)
-    Wb = orc.bf16_round(W)
-    Cp = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
-    out = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    Wh = orc.f16_round(W)
+    Cp = orc.f16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    out = torch.empty(R, H, dtype=H16, device=dev)
     dbp = torch.zeros(R // 128, H, device=dev)  # R / siren_nt_tile rows are written
-    WT = np.ascontiguousarray(Wb.T)
-    ok(lib.siren_inner_bwd_dx(ptr(to_dev(dZ, dev, torch.bfloat16)), ptr(to_dev(WT, dev, torch.bfloat16)),
-                              ptr(to_dev(Cp, dev, torch.bfloat16)), ctypes.c_float(30.0), R, H, ptr(out),
-                              ptr(dbp), S()), lib)
-    ref = (dZ.astype(np.float64) @ Wb.astype(np.float64)) * Cp * 30.0
+    WT = np.ascontiguousarray(Wh.T)
+    ok(lib.siren_inner_bwd_dx(ptr(to_dev(dZ, dev, H16)), ptr(to_dev(WT, dev, H16)),
+                              ptr(to_dev(Cp, dev, H16)), ctypes.c_float(30.0), R, H,
+                              ptr(gscale_dev(dev, k)), ptr(out), ptr(dbp), S()), lib)
+    ref = (dZ.astype(np.float64) @ Wh.astype(np.float64)) * Cp * 30.0
     scale = np.max(np.abs(ref))
-    assert within_bf16(bf16_np(out), ref, 1e-5 * scale) <= 0
-    db = dbp.cpu().numpy().astype(np.float64).sum(0)
+    assert within_f16(f16_np(out), ref, 1e-5 * scale) <= 0
+    db = dbp.cpu().numpy().astype(np.float64).sum(0) * 2.0 ** (k or 0)
     assert np.max(np.abs(db - ref.sum(0))) < 1e-4 * np.max(np.abs(ref.sum(0))) + 1e-6 * scale
 
 
@@ -217,21 +258,22 @@ def test_inner_bwd_dx(lib, dev, R, H, nt_tile):
 def test_first_bwd_dx(lib, dev, in_dim, omega0, nt_tile):
     rng = np.random.default_rng(6)
     R, H = 512, 256
-    dZ1 = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
+    k = 5 if in_dim == 2 else None
+    dZ1 = orc.f16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
     _, W, _ = _inner_inputs(rng, R, H)
-    Wb = orc.bf16_round(W)
+    Wh = orc.f16_round(W)
     t = rng.uniform(-1, 1, (R, in_dim)).astype(F32)
     W0 = rng.uniform(-1 / in_dim, 1 / in_dim, (H, in_dim)).astype(F32)
     b0 = rng.uniform(-1, 1, H).astype(F32)
     part = torch.zeros(R // 128, 1 + in_dim, H, device=dev)
-    WT = np.ascontiguousarray(Wb.T)
+    WT = np.ascontiguousarray(Wh.T)
     A0 = orc.first_preact(t, W0, b0, omega0)
-    C0 = orc.bf16_round(orc.cos32(A0))  # as siren_first_fwd stores it
-    ok(lib.siren_first_bwd_dx(ptr(to_dev(dZ1, dev, torch.bfloat16)), ptr(to_dev(WT, dev, torch.bfloat16)),
-                              ptr(to_dev(C0, dev, torch.bfloat16)), ptr(to_dev(t, dev)), in_dim,
-                              ctypes.c_float(omega0), R, H, ptr(part), S()), lib)
-    dz0 = (dZ1.astype(np.float64) @ Wb.astype(np.float64)) * C0 * omega0
-    got = part.cpu().numpy().astype(np.float64).sum(0)
+    C0 = orc.f16_round(orc.cos32(A0))  # as siren_first_fwd stores it
+    ok(lib.siren_first_bwd_dx(ptr(to_dev(dZ1, dev, H16)), ptr(to_dev(WT, dev, H16)),
+                              ptr(to_dev(C0, dev, H16)), ptr(to_dev(t, dev)), in_dim,
+                              ctypes.c_float(omega0), R, H, ptr(gscale_dev(dev, k)), ptr(part), S()), lib)
+    dz0 = (dZ1.astype(np.float64) @ Wh.astype(np.float64)) * C0 * omega0
+    got = part.cpu().numpy().astype(np.float64).sum(0) * 2.0 ** (k or 0)
     ref_db = dz0.sum(0)
     scale = np.max(np.abs(dz0)) * math.sqrt(R)
     assert np.max(np.abs(got[0] - ref_db)) < 1e-4 * scale
@@ -247,16 +289,18 @@ def test_inner_bwd_dw(lib, dev, R, H, splits, tile, tn_pipe):
     if tile == 128 and tn_pipe != 0:
         pytest.skip("pipeline variants apply to the 256x256 tile")
     rng = np.random.default_rng(7)
-    Y = orc.bf16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
-    dZ = orc.bf16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
+    k = 12 if splits % 2 else None   # odd split counts also check the 1/S of dw_reduce
+    Y = orc.f16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    dZ = orc.f16_round((rng.normal(size=(R, H)) * 1e-3).astype(F32))
     slab = torch.empty(int(lib.siren_slab_floats(H, splits)), device=dev)
     grad = torch.full((H, H), 0.5, device=dev)
-    ok(lib.siren_inner_bwd_dw(ptr(to_dev(Y, dev, torch.bfloat16)), ptr(to_dev(dZ, dev, torch.bfloat16)),
+    ok(lib.siren_inner_bwd_dw(ptr(to_dev(Y, dev, H16)), ptr(to_dev(dZ, dev, H16)),
                               R, H, splits, tile, ptr(slab), S()), lib)
-    ok(lib.siren_dw_reduce(ptr(slab), splits, H, tile, ptr(grad), 1, S()), lib)
-    ref = dZ.astype(np.float64).T @ Y.astype(np.float64) + 0.5
+    ok(lib.siren_dw_reduce(ptr(slab), splits, H, tile, ptr(grad), 1, ptr(gscale_dev(dev, k)), S()), lib)
+    ref = (dZ.astype(np.float64).T @ Y.astype(np.float64)) * 2.0 ** -(k or 0) + 0.5
     got = grad.cpu().numpy().astype(np.float64)
-    assert np.max(np.abs(got - ref)) < 1e-5 * np.max(np.abs(ref - 0.5)) + 1e-7
+    # + one fp32 half-ulp of the 0.5 accumulated into
+    assert np.max(np.abs(got - ref)) < 1e-5 * np.max(np.abs(ref - 0.5)) + 1e-7 * 2.0 ** -(k or 0) + 3e-8
 
 
 def test_col_reduce(lib, dev):
@@ -330,8 +374,8 @@ def test_plateau_trace(lib, dev):
 def test_cast_weight(lib, dev, H):
     rng = np.random.default_rng(11)
     W = rng.normal(size=(H, H)).astype(F32)
-    Wb = torch.empty(H, H, dtype=torch.bfloat16, device=dev)
-    WTb = torch.empty_like(Wb)
-    ok(lib.siren_cast_weight(ptr(to_dev(W, dev)), H, H, ptr(Wb), ptr(WTb), S()), lib)
-    assert np.array_equal(bf16_np(Wb), orc.bf16_round(W))
-    assert np.array_equal(bf16_np(WTb), orc.bf16_round(W).T)
+    Wh = torch.empty(H, H, dtype=H16, device=dev)
+    WTh = torch.empty_like(Wh)
+    ok(lib.siren_cast_weight(ptr(to_dev(W, dev)), H, H, ptr(Wh), ptr(WTh), S()), lib)
+    assert np.array_equal(f16_np(Wh), orc.f16_round(W))
+    assert np.array_equal(f16_np(WTh), orc.f16_round(W).T)
