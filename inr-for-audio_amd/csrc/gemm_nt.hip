@@ -33,19 +33,27 @@
 
 namespace siren {
 
-// Source-side XOR swizzle of a staged [rows][64] h16 image (128-B rows, 8 16-B chunks).
-__device__ __forceinline__ int stage_swz(int r, int c) { return c ^ (r & 7); }
+// Source-side XOR swizzle of a staged [rows][BK] fp16 image (16-B chunks).  BK = 64 (128-B
+// rows, 8 chunks): chunk ^ (row & 7).  BK = 32 (64-B rows, 4 chunks): chunk ^ H[(row>>2)&3]
+// with H = {0,2,3,1}, which makes every 16-lane group of a ds_read_b128 fragment read hit
+// 16 distinct 16-B bank slots.
+template <int BK>
+__device__ __forceinline__ int stage_swz(int r, int c) {
+  if constexpr (BK == 64) return c ^ (r & 7);
+  else return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3);  // H as 2-bit fields of 0x78
+}
 
-template <int BM_, int BN_, int WM_, int WN_>
+template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_>
 struct NtCfg {
-  static constexpr int BM = BM_, BN = BN_, BK = 64;
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, S = S_;
   static constexpr int WM = WM_, WN = WN_, NWAVES = WM_ * WN_, THREADS = 64 * NWAVES;
   static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   static constexpr int SM = TM / 16, SN = TN / 16;  // 16x16 MFMA tiles per wave
   static constexpr int ROWB = BK * 2;               // bytes per staged row
+  static constexpr int RPI = 1024 / ROWB, SPR = ROWB / 16;  // rows / 16-B slots per DMA piece
   static constexpr int XBYTES = BM * ROWB, WBYTES = BN * ROWB;
   static constexpr int STAGE = XBYTES + WBYTES;
-  static constexpr int RING = 2 * STAGE;
+  static constexpr int RING = S * STAGE;
   // epilogue scratch behind the ring: HEAD row partials [WN][BM] or column sums [3][WM][BN],
   // then (NT_FWD) the whole bias and head weight vectors, staged once per block
   static constexpr int RED = 4 * (WN * BM > 3 * WM * BN ? WN * BM : 3 * WM * BN);
@@ -57,8 +65,12 @@ struct NtCfg {
   static_assert(SN % 2 == 0, "16-B row pieces pair adjacent column subtiles");
   static_assert(LDS <= 160 * 1024, "LDS");
 };
-using NtSmall = NtCfg<128, 128, 2, 2>;
-using NtLarge = NtCfg<256, 256, 2, 4>;
+using NtSmall = NtCfg<128, 128, 2, 2, 64, 2>;
+// 256x256 variants (siren_set_option SIREN_OPT_NT_PIPE): BK 64 double buffer (one tile per
+// block, or persistent), BK 32 rings of 4 / 3 slots (persistent)
+using NtLarge = NtCfg<256, 256, 2, 4, 64, 2>;
+using NtLargeR4 = NtCfg<256, 256, 2, 4, 32, 4>;
+using NtLargeR3 = NtCfg<256, 256, 2, 4, 32, 3>;
 
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
@@ -96,19 +108,19 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   };
 
   // ---- LDS-DMA staging addresses -------------------------------------------------
-  // One instruction moves 8 rows x 128 B.  Lane L lands at row L/8, 16-B slot L%8, and
-  // carries the logical chunk stage_swz(row, slot) (source-side swizzle).
-  constexpr int ROWB = Cfg::ROWB;
+  // One instruction moves 1 KiB = RPI rows x ROWB bytes.  Lane L lands at row L/SPR, 16-B
+  // slot L%SPR, and carries the logical chunk stage_swz(row, slot) (source-side swizzle).
+  constexpr int ROWB = Cfg::ROWB, RPI = Cfg::RPI, SPR = Cfg::SPR;
   size_t xrel[Cfg::XINSTR], wrel[Cfg::WINSTR];
 #pragma unroll
   for (int j = 0; j < Cfg::XINSTR; ++j) {
-    const int r = (wave * Cfg::XINSTR + j) * 8 + lane / 8;
-    xrel[j] = (size_t)r * K + stage_swz(r, lane % 8) * 8;
+    const int r = (wave * Cfg::XINSTR + j) * RPI + lane / SPR;
+    xrel[j] = (size_t)r * K + stage_swz<BK>(r, lane % SPR) * 8;
   }
 #pragma unroll
   for (int j = 0; j < Cfg::WINSTR; ++j) {
-    const int r = (wave * Cfg::WINSTR + j) * 8 + lane / 8;
-    wrel[j] = (size_t)r * K + stage_swz(r, lane % 8) * 8;
+    const int r = (wave * Cfg::WINSTR + j) * RPI + lane / SPR;
+    wrel[j] = (size_t)r * K + stage_swz<BK>(r, lane % SPR) * 8;
   }
   auto stage = [&](int ti, int kt, int slot) {
     int m0, n0;
@@ -126,10 +138,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // ---- fragment read offsets --------------------------------------------------------
   // 16x16x32 operand: lane holds row (lane&15), k = 8*(lane>>4) .. +7 of a 32-deep half;
   // fragment rows start at multiples of 16, so the swizzle depends on the lane only.
-  int koff[2];
+  int koff[BK / 32];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-    koff[kk] = (lane & 15) * ROWB + (stage_swz(lane & 15, (lane >> 4) + 4 * kk) << 4);
+  for (int kk = 0; kk < BK / 32; ++kk)
+    koff[kk] = (lane & 15) * ROWB + (stage_swz<BK>(lane & 15, (lane >> 4) + 4 * kk) << 4);
   auto frags = [&](int slot, int kk, h16x8 (&A)[SN], h16x8 (&B)[SM]) {
     const char* xs = smem + slot * Cfg::STAGE;
     const char* ws = xs + Cfg::XBYTES;
@@ -332,7 +344,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     }
   };
 
-  mfma_pipeline_tiles<2, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
+  mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
       my_tiles, K / BK, acc, stage, frags, pre, epilogue, p.stamps);
 }
 
@@ -378,8 +390,9 @@ static hipError_t dispatch_mode(int mode, bool head, const NtParams& p, hipStrea
   return hipErrorInvalidValue;
 }
 
-// tile override for A/B measurement: 0 = auto, 128 or 256; pipe: 1 = persistent 256x256
-// (default), 0 = one tile per block
+// tile override for A/B measurement: 0 = auto, 128 or 256; pipe (256x256): 0 = BK 64, one
+// tile per block; 1 = BK 64 persistent (default); 2 = BK 32 4-slot ring persistent;
+// 3 = BK 32 3-slot ring persistent
 static int g_nt_tile = 0;
 static int g_nt_pipe = 1;
 void gemm_nt_set_tile(int tile) { g_nt_tile = tile; }
@@ -398,7 +411,12 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (mode == NT_DX0 && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
   if (p.tile == 256) {
     if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
-    return dispatch_mode<NtLarge>(mode, head, p, s, g_nt_pipe != 0);
+    switch (g_nt_pipe) {
+      case 0: return dispatch_mode<NtLarge>(mode, head, p, s, false);
+      case 2: return dispatch_mode<NtLargeR4>(mode, head, p, s, true);
+      case 3: return dispatch_mode<NtLargeR3>(mode, head, p, s, true);
+      default: return dispatch_mode<NtLarge>(mode, head, p, s, true);
+    }
   }
   if (p.tile != 128) return hipErrorInvalidValue;
   return dispatch_mode<NtSmall>(mode, head, p, s, false);

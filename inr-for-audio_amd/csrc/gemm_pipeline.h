@@ -115,19 +115,19 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-// Persistent variant for short-K GEMMs (K = hidden width, 16 K-steps per tile): the block
-// walks `ntiles` tiles and the double-buffered ring runs straight across tile boundaries.
+// Persistent S-slot ring for short-K GEMMs (K = hidden width): the block walks `ntiles`
+// tiles and the ring runs straight across tile boundaries, S-1 stages ahead.
 // vmcnt retires loads AND stores in issue order (MI355X_MICROARCH.md §vmcnt), so a stage
 // issued after an epilogue's stores cannot be waited for without waiting for the stores too.
-// Hence at a tile boundary BOTH first stages of the next tile are issued before the
-// epilogue runs: stage k0 at the top of the last K-step as usual, stage k1 into the slot the
-// last K-step just read (one extra barrier per tile).  The next tile's K-steps 0 and 1 then
-// wait with vmcnt(G + SLACK) and vmcnt(SLACK) -- the stores keep draining under two K-steps
-// of MFMAs -- and only K-step 2 waits for them.
+// The stages already in flight when an epilogue issues its stores are therefore waited for
+// with SLACK more outstanding operations allowed (the stores drain under those K-steps); a
+// wait for a stage issued after the stores is strict.  With S = 2 only one stage would be
+// in flight, so the second stage of the next tile is issued early, into the slot the last
+// K-step just read (one extra barrier per tile), before the epilogue.
 //   stage(tile, kt, slot)  issues the LDS-DMA of K-step kt of the block's tile-th tile;
 //   frags(slot, kk, A, B)  reads one k32 half of the operand fragments;
-//   pre(tile)              issues the epilogue's own global loads (bias, Cprev, ...) BEFORE
-//                          the early prefetch, so that waiting for them does not wait for it;
+//   pre(tile)              issues the epilogue's own global loads (Cprev, ...) before the
+//                          S = 2 early prefetch, so that waiting for them does not wait for it;
 //   epi(tile)              consumes acc; the ring is NOT available to it (own LDS scratch;
 //                          raw barriers only -- every wave calls epi the same number of times).
 // SLACK = vector-memory instructions every wave's epilogue issues (a lower bound; 0 is always
@@ -143,13 +143,30 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 }
 #endif
 
-template <int KK, int G, int NA, int NB, int SLACK, class StageFn, class FragFn, class PreFn,
+// s_waitcnt vmcnt(G*y + (relaxed ? SLACK : 0)) for a wave-uniform y in [0, J]
+template <int G, int SLACK, int J>
+__device__ __forceinline__ void wait_stage(int y, bool relaxed) {
+  if constexpr (J >= 0) {
+    if (y == J) {
+      if (relaxed) wait_vmcnt<G * J + SLACK>();
+      else wait_vmcnt<G * J>();
+      return;
+    }
+    wait_stage<G, SLACK, J - 1>(y, relaxed);
+  } else {
+    wait_vmcnt<0>();
+  }
+}
+
+template <int S, int KK, int G, int NA, int NB, int SLACK, class StageFn, class FragFn, class PreFn,
           class EpiFn>
 __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&acc)[NA][NB],
                                                     StageFn&& stage, FragFn&& frags, PreFn&& pre,
                                                     EpiFn&& epi,
                                                     unsigned long long* stamps = nullptr) {
-  static_assert(SLACK >= 0 && G + SLACK < 64, "vmcnt immediate");
+  static_assert(S >= 2 && S <= 6, "ring depth");
+  constexpr int YMAX = (S == 2) ? 1 : S - 2;  // younger stages in flight at a wait
+  static_assert(SLACK >= 0 && G * YMAX + SLACK < 64, "vmcnt immediate");
   const int total = ntiles * nk;
   if (total <= 0) return;
 #ifdef SIREN_NT_STAMPS
@@ -162,23 +179,27 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
 #endif
   int it = 0, ik = 0;  // issue pointer (tile, K-step)
   int issued = 0;      // stages issued so far (global step index of the next one)
-  auto issue = [&](int slot) {
-    stage(it, ik, slot);
+  int fill = 0;        // ring slot of the next stage
+  auto issue = [&]() {
+    stage(it, ik, fill);
     if (++ik == nk) { ik = 0; ++it; }
     ++issued;
+    fill = (fill + 1 == S) ? 0 : fill + 1;
   };
-  issue(0);
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (issued < total) issue();
   int ct = 0, ck = 0, slot = 0;
-  int after = 0;  // 1: first K-step after an epilogue with the early prefetch, 2: second
+  int relax = 0;  // K-steps left whose stage was issued before the last epilogue's stores
   for (int u = 0; u < total; ++u) {
     SIREN_STAMP(st_a = stamp_now(); if (ck == 0) { st_tile = st_a; st_wait = 0; })
-    if (after == 1) wait_vmcnt<G + SLACK>();
-    else if (after == 2) wait_vmcnt<SLACK>();
-    else wait_vmcnt<0>();
+    wait_stage<G, SLACK, YMAX>(issued - (u + 1), relax > 0);
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     SIREN_STAMP(st_wait += stamp_now() - st_a;)
-    if (issued == u + 1 && issued < total) issue(slot ^ 1);
+    if (relax > 0) --relax;
+    // stage u+S-1 goes into the slot K-step u-1 read (every wave is past the barrier)
+    if (issued < total && issued < u + S) issue();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
@@ -191,17 +212,14 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[i], B[j], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
-    after = (after == 1) ? 2 : 0;
     if (++ck == nk) {
       SIREN_STAMP(const unsigned long long st_c = stamp_now();)
       pre(ct);
-      if (issued == u + 2 && issued < total) {
-        lds_barrier();  // every wave is done reading `slot`
-        issue(slot);
-        after = 1;
-      } else {
-        after = 2;      // only the (older) next stage is outstanding besides the stores
+      if (S == 2 && issued == u + 2 && issued < total) {
+        lds_barrier();  // every wave is done reading `slot` (== fill)
+        issue();
       }
+      relax = issued - (u + 1);  // stages in flight ahead of the stores
       epi(ct);
       SIREN_STAMP(if (st_on && ct < 256) {
         const unsigned long long st_d = stamp_now();
@@ -217,7 +235,7 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
       ck = 0;
       ++ct;
     }
-    slot ^= 1;
+    slot = (slot + 1 == S) ? 0 : slot + 1;
   }
   wait_vmcnt<0>();
   wait_lgkm0();

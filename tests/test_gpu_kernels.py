@@ -50,7 +50,8 @@ def _release():
     _KEEP.clear()
 
 
-@pytest.fixture(params=[(128, 0, 0), (256, 0, 0), (256, 1, 0), (256, 1, 2)],
+@pytest.fixture(params=[(128, 0, 0), (256, 0, 0), (256, 1, 0), (256, 1, 2), (256, 2, 0), (256, 2, 2),
+                        (256, 3, 3)],
                 ids=lambda p: f"t{p[0]}p{p[1]}g{p[2]}")
 def nt_tile(request, lib):
     """Force the NT GEMM tile edge, persistence and persistent grid size (siren_set_option)

@@ -70,7 +70,7 @@ def main():
     R, H = args.rows, args.hidden
     s = torch.cuda.current_stream().cuda_stream
     P = lambda t: t.data_ptr()  # noqa: E731
-    bf = torch.bfloat16
+    bf = torch.float16
     g = torch.Generator(device=dev).manual_seed(0)
     X = (torch.rand(R, H, device=dev, generator=g) * 2 - 1).to(bf)
     lim = math.sqrt(6 / H) / 30
@@ -84,8 +84,8 @@ def main():
     t = torch.linspace(-1, 1, R, device=dev).reshape(R, 1)
     cases = {
         "fwd": lambda: lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), None, None, s),
-        "dx": lambda: lib.siren_inner_bwd_dx(P(dZ), P(W), P(C), ctypes.c_float(30.0), R, H, P(dZp), P(part), s),
-        "dx0": lambda: lib.siren_first_bwd_dx(P(dZ), P(W), P(C), P(t), 1, ctypes.c_float(3000.0), R, H, P(part), s),
+        "dx": lambda: lib.siren_inner_bwd_dx(P(dZ), P(W), P(C), ctypes.c_float(30.0), R, H, None, P(dZp), P(part), s),
+        "dx0": lambda: lib.siren_first_bwd_dx(P(dZ), P(W), P(C), P(t), 1, ctypes.c_float(3000.0), R, H, None, P(part), s),
     }
     lib.siren_set_option(5, args.stagger)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count

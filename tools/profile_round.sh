@@ -1,0 +1,23 @@
+#!/usr/bin/env bash
+# Round profile on the GPU box (run through gpurun from the repo root):
+#   bench.json              the default bench line (incl. cpu_baseline)
+#   trace/                  rocprofv3 --kernel-trace --stats of a short bench run
+#   bench_pmc_hbm.json      FETCH_SIZE and WRITE_SIZE, each in its own --pmc pass
+# Every GPU step has its own time limit and the steps are chained with &&.
+#   bash tools/profile_round.sh r02
+set -euo pipefail
+TAG=${1:?round tag, e.g. r02}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+python3 "$ROOT/__graft_entry__.py"
+timeout -k 10 400 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+  python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/trace.log" 2>&1 &&
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1 &&
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1 &&
+python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_hbm.json" "$OUT/pmc_fetch" "$OUT/pmc_write"
+echo "profile $TAG done"
