@@ -279,7 +279,7 @@ int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float
                     int32_t rows, int32_t hidden, uint16_t* Y0, uint16_t* C0, void* stream) {
   if (!t || !W0 || !b0 || !Y0 || !C0) return SIREN_ERR_NULL;
   if (in_dim < 1 || in_dim > 2) return SIREN_ERR_CONFIG;
-  if (rows < 0 || hidden % 4) return SIREN_ERR_SHAPE;
+  if (rows < 0 || hidden < 8 || hidden > 2048 || hidden % 8 || 256 % (hidden / 8)) return SIREN_ERR_SHAPE;
   return (int)first_fwd(t, in_dim, W0, b0, omega0, rows, hidden, B(Y0), B(C0), S(stream));
 }
 

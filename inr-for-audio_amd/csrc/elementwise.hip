@@ -41,37 +41,64 @@ hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, 
 // ---------------------------------------------------------------------------------
 // First SineLayer (is_first=True, models.py:105-115): y0 = sin(omega0 * (t W0^T + b0)).
 // Kept in fp32 end to end: |omega0*z| reaches ~4.4e4 rad at omega0 = 22000, so the
-// pre-activation is formed exactly as torch's CPU addmm rounds it (K=1: one fma;
-// K=2: fma(t1, w1, t0*w0) + b) and sinf does a full-precision range reduction.
+// pre-activation a is formed exactly as torch's CPU addmm rounds it (K=1: one fma;
+// K=2: fma(t1, w1, t0*w0) + b), then reduced in revolutions with a two-part 1/(2*pi):
+//   r = fma(a, inv2pi_hi, -n) + a * inv2pi_lo,  n = rint(a * inv2pi_hi)
+// fma forms a*inv2pi_hi - n with one rounding (|r| <= 1/2: error <= 2^-25 rev), the low part
+// adds < 2e-4 rev with 2^-24 relative error, so r is within ~4e-8 rev (2.5e-7 rad) of a/(2pi)
+// mod 1 for every |a| < 2^17.  v_sin_f32 / v_cos_f32 take revolutions directly.  (OCML's
+// sincosf with its large-argument reduction made this kernel VALU-bound at 2.1 ms.)
+__device__ __forceinline__ void sincos_rev(float a, float* s, float* c) {
+  constexpr float kHi = 0x1.45f306p-3f;  // fp32(1/(2*pi))             0x3E22F983
+  constexpr float kLo = 0x1.b93910p-28f; // fp32(1/(2*pi) - kHi) = 6.42e-9  0x31DC9C88
+  const float n = __builtin_rintf(a * kHi);
+  const float r = __builtin_fmaf(a, kLo, __builtin_fmaf(a, kHi, -n));
+  *s = __builtin_amdgcn_sinf(r);
+  *c = __builtin_amdgcn_cosf(r);
+}
+// Row-wise: each thread owns 8 columns (W0 / b0 in registers) and walks rows; a row is H/8
+// threads, a 256-thread block covers 256/(H/8) rows per pass; Y0 / C0 go out as 16-B pieces.
 __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const float* __restrict__ W0,
                                  const float* __restrict__ b0, float omega0, int R, int H,
                                  h16* __restrict__ Y0, h16* __restrict__ C0) {
-  const int hq = H >> 2;
-  const int64_t total = (int64_t)R * hq;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = idx / hq;
-    const int n = (int)(idx - m * hq) * 4;
+  const int tpr = H >> 3;
+  const int rpb = blockDim.x / tpr;
+  const int lt = threadIdx.x % tpr, lr = threadIdx.x / tpr;
+  const int n = lt * 8;
+  float w0[8], w1[8], bb[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    w0[r] = W0[(n + r) * in_dim];
+    w1[r] = (in_dim > 1) ? W0[(n + r) * in_dim + 1] : 0.f;
+    bb[r] = b0[n + r];
+  }
+  for (int64_t m = (int64_t)blockIdx.x * rpb + lr; m < R; m += (int64_t)gridDim.x * rpb) {
     const float t0 = t[m * in_dim];
     const float t1 = (in_dim > 1) ? t[m * in_dim + 1] : 0.f;
-    float y[4], c[4];
+    float y[8], c[8];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float z;
-      if (in_dim == 1) z = __builtin_fmaf(t0, W0[n + r], b0[n + r]);
-      else z = __builtin_fmaf(t1, W0[(n + r) * 2 + 1], t0 * W0[(n + r) * 2]) + b0[n + r];
-      sincosf(omega0 * z, &y[r], &c[r]);
+    for (int r = 0; r < 8; ++r) {
+      const float z = (in_dim == 1) ? __builtin_fmaf(t0, w0[r], bb[r])
+                                    : __builtin_fmaf(t1, w1[r], t0 * w0[r]) + bb[r];
+      sincos_rev(omega0 * z, &y[r], &c[r]);
     }
-    *(h16x4*)(Y0 + m * H + n) = pack4(y[0], y[1], y[2], y[3]);
-    *(h16x4*)(C0 + m * H + n) = pack4(c[0], c[1], c[2], c[3]);
+    h16x8 yv, cv;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      yv[r] = (h16)y[r];
+      cv[r] = (h16)c[r];
+    }
+    *(h16x8*)(Y0 + m * H + n) = yv;
+    *(h16x8*)(C0 + m * H + n) = cv;
   }
 }
 
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
                      int R, int H, h16* Y0, h16* C0, hipStream_t s) {
-  if (H % 4 || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(first_fwd_kernel, dim3(grid_for((int64_t)R * (H / 4), 256)), dim3(256), 0, s, t,
-                     in_dim, W0, b0, omega0, R, H, Y0, C0);
+  if (H % 8 || H > 2048 || 256 % (H / 8) || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
+  const int rpb = 256 / (H / 8);
+  hipLaunchKernelGGL(first_fwd_kernel, dim3(grid_for(R, rpb, 4096)), dim3(256), 0, s, t, in_dim, W0, b0,
+                     omega0, R, H, Y0, C0);
   return hipGetLastError();
 }
 
