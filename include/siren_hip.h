@@ -197,9 +197,10 @@ enum siren_prof_kind {
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
  * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;
  * SIREN_OPT_NT_PIPE = 256x256 NT GEMM variant: 0 BK 64 one tile per block, 1 BK 64
- * persistent (default), 2 BK 32 4-slot ring persistent, 3 BK 32 3-slot ring persistent;
- * SIREN_OPT_TN_PIPE = 0..2 selects the 256x256 dW K-loop (0: BK 64 double buffer
- * (default), 1: BK 32 4-slot ring, 2: BK 32 5-slot ring);
+ * persistent (default), 2 BK 32 4-slot ring persistent, 3 BK 32 3-slot ring persistent,
+ * 4 BK 64 persistent with two wave groups in ping-pong;
+ * SIREN_OPT_TN_PIPE = 0..3 selects the 256x256 dW K-loop (0: BK 64 double buffer
+ * (default), 1: BK 32 4-slot ring, 2: BK 32 5-slot ring, 3: BK 64 ping-pong);
  * SIREN_OPT_NT_GRID = persistent NT grid size (0 = one block per CU; tests use small
  * values so every block walks several tiles);
  * SIREN_OPT_NT_STAGGER = persistent NT start stagger: block b idles (b % 16) * value units of

@@ -43,9 +43,10 @@ __device__ __forceinline__ int stage_swz(int r, int c) {
   else return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3);  // H as 2-bit fields of 0x78
 }
 
-template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_>
+template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_, bool PP_ = false>
 struct NtCfg {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, S = S_;
+  static constexpr bool PP = PP_;  // ping-pong K-loop (gemm_pipeline.h pingpong_tiles)
   static constexpr int WM = WM_, WN = WN_, NWAVES = WM_ * WN_, THREADS = 64 * NWAVES;
   static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   static constexpr int SM = TM / 16, SN = TN / 16;  // 16x16 MFMA tiles per wave
@@ -71,6 +72,8 @@ using NtSmall = NtCfg<128, 128, 2, 2, 64, 2>;
 using NtLarge = NtCfg<256, 256, 2, 4, 64, 2>;
 using NtLargeR4 = NtCfg<256, 256, 2, 4, 32, 4>;
 using NtLargeR3 = NtCfg<256, 256, 2, 4, 32, 3>;
+// BK 64 double buffer, persistent, two wave groups in ping-pong (SIREN_OPT_NT_PIPE 4)
+using NtLargePP = NtCfg<256, 256, 2, 4, 64, 2, true>;
 
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
@@ -91,6 +94,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   const int K = p.K, N = p.N;
   const int tiles_n = N / BN;
   const int ntiles = (p.M / BM) * tiles_n;
+  const bool tn_pow2 = (tiles_n & (tiles_n - 1)) == 0;  // N / BN is 1, 2, 4 or 8 at H <= 1024
+  const int tn_shift = __builtin_ctz(tiles_n);
   // Block b takes tiles b', b'+G, ... with b' the XCD-grouped id: the G/8 blocks of one XCD
   // hold consecutive tile ids, i.e. they share X row-blocks in L2 at the same time.
   const int G = gridDim.x;
@@ -102,7 +107,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   for (int i = (bp & 15) * p.stagger; i > 0; --i) __builtin_amdgcn_s_sleep(27);
   auto tile_of = [&](int i, int& m0, int& n0) {
     const int g = bp + i * G;
-    const int tm = g / tiles_n;
+    const int tm = tn_pow2 ? (g >> tn_shift) : g / tiles_n;
     m0 = tm * BM;
     n0 = (g - tm * tiles_n) * BN;
   };
@@ -344,8 +349,86 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     }
   };
 
-  mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
-      my_tiles, K / BK, acc, stage, frags, pre, epilogue, p.stamps);
+  if constexpr (Cfg::PP) {
+    static_assert(BM == 256 && BN == 256 && BK == 64 && Cfg::WM == 2 && WN == 4, "ping-pong geometry");
+    const int nk = K / BK;
+    // Staging pieces of a K-tile (16 KiB, 2 LDS-DMA per wave; 8 rows x 128 B per instruction):
+    //   pc 0: W rows wn*64 + 0..31   (phase a)      pc 1: X rows wm*128 + 0..63   (phase a)
+    //   pc 2: W rows wn*64 + 32..63  (phase b)      pc 3: X rows wm*128 + 64..127 (phases c)
+    // Phases (m half, n half) of every wave's 128x64 tile: a (0,0), b (0,1), c (1,1), d (1,0).
+    int psrc[4][2];
+    unsigned pdst[4][2];
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int pr0 = (2 * wave + j) * 8, hf = pc >> 1;
+        const int lr0 = (pc & 1) ? (pr0 >> 6) * 128 + (pr0 & 63) + 64 * hf
+                                 : (pr0 >> 5) * 64 + (pr0 & 31) + 32 * hf;
+        const int lr = lr0 + (lane >> 3);
+        psrc[pc][j] = lr * K + stage_swz<BK>(lr, lane & 7) * 8;
+        pdst[pc][j] = ((pc & 1) ? 0u : (unsigned)Cfg::XBYTES) + (unsigned)(lr0 * ROWB);
+      }
+    auto issue = [&](int ti, int kt, int slot, auto pcc) -> bool {
+      constexpr int PC = decltype(pcc)::value;
+      if (ti >= my_tiles) return false;
+      int m0, n0;
+      tile_of(ti, m0, n0);
+      const h16* src = ((PC & 1) ? p.X + (size_t)m0 * K : p.W + (size_t)n0 * K) + kt * BK;
+      const char* dst = smem + slot * Cfg::STAGE;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) glds16_asm(src + psrc[PC][j], lds_addr(dst + pdst[PC][j]));
+      return true;
+    };
+    h16x8 xf[4][2], wf0[2][2], wf1[2][2];
+    auto rd_w = [&](h16x8 (&wf)[2][2], const char* ws, int n_off) {
+#pragma unroll
+      for (int il = 0; il < 2; ++il)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          wf[il][kk] = *(const h16x8*)(ws + (wn * TN + n_off + il * 16) * ROWB + koff[kk]);
+    };
+    auto read = [&](auto ph, int slot) {
+      constexpr int PH = decltype(ph)::value;
+      const char* xs = smem + slot * Cfg::STAGE;
+      const char* ws = xs + Cfg::XBYTES;
+      if constexpr (PH == 0 || PH == 2) {
+#pragma unroll
+        for (int jl = 0; jl < 4; ++jl)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            xf[jl][kk] = *(const h16x8*)(xs + (wm * TM + (PH == 2 ? 64 : 0) + jl * 16) * ROWB + koff[kk]);
+      }
+      if constexpr (PH == 0) rd_w(wf0, ws, 0);
+      if constexpr (PH == 1) rd_w(wf1, ws, 32);
+    };
+    auto mma = [&](auto ph) {
+      constexpr int PH = decltype(ph)::value;
+      constexpr int MH = PH >> 1, NH = (PH == 1 || PH == 2) ? 1 : 0;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int il = 0; il < 2; ++il)
+#pragma unroll
+          for (int jl = 0; jl < 4; ++jl) {
+            const h16x8 a = NH ? wf1[il][kk] : wf0[il][kk];
+            acc[2 * NH + il][4 * MH + jl] =
+                __builtin_amdgcn_mfma_f32_16x16x32_f16(a, xf[jl][kk], acc[2 * NH + il][4 * MH + jl], 0, 0, 0);
+          }
+    };
+    auto tile_end = [&](int ti) {
+      pre(ti);
+      epilogue(ti);
+#pragma unroll
+      for (int i = 0; i < SN; ++i)
+#pragma unroll
+        for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(my_tiles, nk, wm, issue, read, mma, tile_end);
+  } else {
+    mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
+        my_tiles, K / BK, acc, stage, frags, pre, epilogue, p.stamps);
+  }
 }
 
 static int g_num_cus = 0;
@@ -392,7 +475,7 @@ static hipError_t dispatch_mode(int mode, bool head, const NtParams& p, hipStrea
 
 // tile override for A/B measurement: 0 = auto, 128 or 256; pipe (256x256): 0 = BK 64, one
 // tile per block; 1 = BK 64 persistent (default); 2 = BK 32 4-slot ring persistent;
-// 3 = BK 32 3-slot ring persistent
+// 3 = BK 32 3-slot ring persistent; 4 = BK 64 persistent ping-pong (pingpong_tiles)
 static int g_nt_tile = 0;
 static int g_nt_pipe = 1;
 void gemm_nt_set_tile(int tile) { g_nt_tile = tile; }
@@ -415,6 +498,7 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
       case 0: return dispatch_mode<NtLarge>(mode, head, p, s, false);
       case 2: return dispatch_mode<NtLargeR4>(mode, head, p, s, true);
       case 3: return dispatch_mode<NtLargeR3>(mode, head, p, s, true);
+      case 4: return dispatch_mode<NtLargePP>(mode, head, p, s, true);
       default: return dispatch_mode<NtLarge>(mode, head, p, s, true);
     }
   }

@@ -14,6 +14,7 @@
 // (cdna_hip_programming.md §5 "Pipelining across barriers"); all LDS lives in ONE __shared__
 // array so hipcc does not insert a vmcnt(0) before every ds_read (§5 item 4a).
 #pragma once
+#include <type_traits>
 #include "siren_common.h"
 
 namespace siren {
@@ -241,6 +242,124 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
   wait_lgkm0();
   __builtin_amdgcn_s_barrier();
 #undef SIREN_STAMP
+}
+
+// ---- Ping-pong K-loop of the 256x256 / 8-wave GEMMs ----------------------------------------
+// (cdna_hip_programming.md §5, "The 256² 8-phase template": T2+T3+T4+T5.)  The 8 waves form two
+// groups of 4 (grp = wave >> 2) that run ONE BARRIER APART: on every SIMD one wave issues its
+// 16-MFMA cluster while its partner (the other group) issues LDS reads and LDS-DMA.  A K-tile
+// (BK = 64) is 4 phases a, b, c, d; each phase is
+//     MEM:  ds_read this phase's fragments; issue one staging piece (16 KiB = 2 LDS-DMA per
+//           wave); [counted vmcnt]
+//     s_barrier; lgkmcnt(0); setprio 1; 16 MFMA; setprio 0; s_barrier
+// Group 1 executes one extra s_barrier first, so group 0's MFMA cluster runs between the same
+// two barrier instances as group 1's MEM section and vice versa.
+//
+// Staging: 2 LDS slots (slot = K-tile & 1), each K-tile in 4 pieces pc 0..3.  Phase a of
+// K-tile u issues pc 2 of u+1, b: pc 3 of u+1, c: pc 0 of u+2, d: pc 1 of u+2 (so the pieces
+// of K-tile k go out at global phases 4k-6 .. 4k-3).  With the stagger, every wave's vmcnt in
+// phase r precedes a barrier instance that every wave passes before its MEM section of phase
+// r+1 (RAW), and a ds_read of phase q is retired (lgkmcnt(0)) before a barrier every wave
+// passes before its MEM section of phase q+2 (WAR).  Hence the caller's contract:
+//   last ds_read of pc 0 in phase <= a, pc 1 <= b, pc 2 <= c, pc 3 <= d   (WAR)
+//   first ds_read of pc 0, pc 1 >= a (wait in d); pc 2 >= b (wait in a, or in b when first
+//   read in c); pc 3 >= c (wait in b)                                      (RAW)
+// WAITMASK bit PH = phase PH waits.  A wait lets the pieces of phases r-3..r stay in flight
+// (`hist` records which phases issued one), i.e. piece r-4 has landed.  A tile's epilogue
+// (tile_end) issues >= E stores after the pieces then in flight; the waits of the next tile's
+// first K-tile (whose awaited piece is older than those stores) count them as in flight too.
+//   issue(ti, kt, slot, phase_t<PC>) -> bool   LDS-DMA of piece PC of K-step kt of the block's
+//                                   tile ti into LDS slot `slot` (false: ti past the last tile)
+//   read(phase_t<PH>, slot)         this wave's fragments for phase PH
+//   mma(phase_t<PH>)                its 16 MFMAs
+//   tile_end(ti)                    epilogue with both groups aligned (equal barrier count)
+template <int PH>
+using phase_t = std::integral_constant<int, PH>;
+
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");  // no LDS access moves across the barrier
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int E>
+__device__ __forceinline__ void pp_wait(unsigned hist, bool relaxed) {
+  const int y = __builtin_popcount(hist & 15u);  // pieces issued in phases r-3..r
+  if (relaxed) {
+    switch (y) {
+      case 4: wait_vmcnt<8 + E>(); break;
+      case 3: wait_vmcnt<6 + E>(); break;
+      case 2: wait_vmcnt<4 + E>(); break;
+      case 1: wait_vmcnt<2 + E>(); break;
+      default: wait_vmcnt<E>(); break;
+    }
+  } else {
+    switch (y) {
+      case 4: wait_vmcnt<8>(); break;
+      case 3: wait_vmcnt<6>(); break;
+      case 2: wait_vmcnt<4>(); break;
+      case 1: wait_vmcnt<2>(); break;
+      default: wait_vmcnt<0>(); break;
+    }
+  }
+}
+
+template <int E, int WAITMASK, class IssueFn, class ReadFn, class MmaFn, class EndFn>
+__device__ __forceinline__ void pingpong_tiles(int ntiles, int nk, int grp, IssueFn&& issue,
+                                               ReadFn&& read, MmaFn&& mma, EndFn&& tile_end) {
+  static_assert(E >= 0 && 8 + E < 64, "vmcnt immediate");
+  if (ntiles * nk <= 0) return;
+  // (tile, K-step) of the K-tiles u+1 and u+2, advanced incrementally (scalar, no division)
+  auto next = [&](int& t, int& k) {
+    if (++k == nk) { k = 0; ++t; }
+  };
+  int t1 = 0, k1 = 0, t2, k2;
+  next(t1, k1);
+  t2 = t1, k2 = k1;
+  next(t2, k2);
+  unsigned hist = 0;  // bit i: a piece was issued i phases ago
+  hist = (hist << 1) | (unsigned)issue(0, 0, 0, phase_t<0>{});
+  hist = (hist << 1) | (unsigned)issue(0, 0, 0, phase_t<1>{});
+  hist = (hist << 1) | (unsigned)issue(0, 0, 0, phase_t<2>{});
+  hist = (hist << 1) | (unsigned)issue(0, 0, 0, phase_t<3>{});
+  hist = (hist << 1) | (unsigned)issue(t1, k1, 1, phase_t<0>{});
+  hist = (hist << 1) | (unsigned)issue(t1, k1, 1, phase_t<1>{});
+  pp_wait<0>(hist, false);  // this wave's share of K-tile 0's pieces 0, 1 has landed
+  wait_lgkm0();
+  pp_barrier();             // ... every wave's
+  if (grp) pp_barrier();    // group 1 runs one barrier behind
+  int u = 0;
+  for (int ti = 0; ti < ntiles; ++ti) {
+    for (int kt = 0; kt < nk; ++kt, ++u) {
+      const bool relaxed = (kt == 0) && (ti > 0);
+      const int slot = u & 1;
+      auto phase = [&](auto ph) {
+        constexpr int PH = decltype(ph)::value;
+        read(ph, slot);
+        if constexpr (PH < 2) hist = (hist << 1) | (unsigned)issue(t1, k1, slot ^ 1, phase_t<PH + 2>{});
+        else hist = (hist << 1) | (unsigned)issue(t2, k2, slot, phase_t<PH - 2>{});
+        if constexpr (((WAITMASK >> PH) & 1) != 0) pp_wait<E>(hist, relaxed);
+        pp_barrier();
+        wait_lgkm0();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        mma(ph);
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+      };
+      phase(phase_t<0>{});
+      phase(phase_t<1>{});
+      phase(phase_t<2>{});
+      phase(phase_t<3>{});
+      t1 = t2, k1 = k2;
+      next(t2, k2);
+    }
+    if (grp == 0) pp_barrier();                     // meet group 1's last barrier: aligned
+    tile_end(ti);
+    if (grp == 1 && ti + 1 < ntiles) pp_barrier();  // group 1 one barrier behind again
+  }
+  wait_vmcnt<0>();
 }
 
 }  // namespace siren

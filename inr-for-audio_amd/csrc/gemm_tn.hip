@@ -19,9 +19,10 @@
 
 namespace siren {
 
-template <int BI_, int BJ_, int WM_, int WN_, int BK_ = 64, int S_ = 2>
+template <int BI_, int BJ_, int WM_, int WN_, int BK_ = 64, int S_ = 2, bool PP_ = false>
 struct TnCfg {
   static constexpr int BI = BI_, BJ = BJ_, BK = BK_, S = S_;
+  static constexpr bool PP = PP_;  // ping-pong K-loop (gemm_pipeline.h pingpong_tiles)
   static constexpr int WM = WM_, WN = WN_, NWAVES = WM_ * WN_, THREADS = 64 * NWAVES;
   static constexpr int TI = BI / WM, TJ = BJ / WN, SI = TI / 16, SJ = TJ / 16;
   static constexpr int YROW = BI * 2, ZROW = BJ * 2;       // bytes per staged row
@@ -37,6 +38,7 @@ using TnLarge = TnCfg<256, 256, 2, 4>;          // slab geometry of every 256x25
 using TnL0 = TnCfg<256, 256, 2, 4, 64, 2>;      // BK 64, double buffer
 using TnL1 = TnCfg<256, 256, 2, 4, 32, 4>;      // BK 32, 4-slot ring
 using TnL2 = TnCfg<256, 256, 2, 4, 32, 5>;      // BK 32, 5-slot ring
+using TnLPP = TnCfg<256, 256, 2, 4, 64, 2, true>;  // BK 64, two wave groups in ping-pong
 
 // Chunk swizzle of a staged [64][cols] image: physical 16-B chunk = c ^ f(r).  With
 // h(r) = (r&3) | ((r>>3)&1)<<2 and f = 2h, the 8 rows a 32-lane half touches in one
@@ -129,7 +131,65 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
 #pragma unroll
     for (int s = 0; s < SJ; ++s) B[s] = tr_frag<ZROW>(zs + kk * 32 * ZROW + colB[s]);
   };
-  mfma_pipeline<Cfg::S, false, BK / 32, Cfg::YINSTR + Cfg::ZINSTR>(ks_end - ks_begin, acc, stage, frags);
+  if constexpr (Cfg::PP) {
+    static_assert(Cfg::BI == 256 && Cfg::BJ == 256 && BK == 64 && Cfg::WM == 2 && Cfg::WN == 4,
+                  "ping-pong geometry");
+    // Staging pieces of a K-tile (64 coordinates; 16 KiB = 2 LDS-DMA per wave, 2 rows of 512 B
+    // per instruction): pc 0 = dZ rows 0..31, pc 1 = Y rows 0..31, pc 2 = dZ rows 32..63,
+    // pc 3 = Y rows 32..63.  Phases (k32 half, i half): a (0,0), b (0,1), c (1,1), d (1,0), so
+    // pc 0 is read in a, pc 1 in a-b, pc 2 in c, pc 3 in c-d (pingpong_tiles contract).
+    int yo[2][2], zo[2][2];
+    unsigned po[2][2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r0 = 32 * kk + 4 * wave + 2 * j, r = r0 + (lane >> 5);
+        const int ch = ((lane & 31) ^ tn_swz(r)) * 8;
+        yo[kk][j] = r * p.Hin + k0 + ch;
+        zo[kk][j] = r * p.Hout + o0 + ch;
+        po[kk][j] = (unsigned)(r0 * YROW);
+      }
+    const int nkl = ks_end - ks_begin;
+    auto issue = [&](int ti, int kt, int slot, auto pcc) -> bool {
+      constexpr int PC = decltype(pcc)::value, KK = PC >> 1;
+      if (ti > 0) return false;
+      const int ks = ks_begin + kt;
+      const char* dst = smem + slot * Cfg::STAGE;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if constexpr ((PC & 1) != 0)
+          glds16_asm(p.Y + (size_t)ks * BK * p.Hin + yo[KK][j], lds_addr(dst + po[KK][j]));
+        else
+          glds16_asm(p.dZ + (size_t)ks * BK * p.Hout + zo[KK][j], lds_addr(dst + Cfg::YBYTES + po[KK][j]));
+      }
+      return true;
+    };
+    h16x8 af[4], bf[4];
+    auto read = [&](auto ph, int slot) {
+      constexpr int PH = decltype(ph)::value, KK = PH >> 1, IH = (PH == 1 || PH == 2) ? 1 : 0;
+      const char* ys = smem + slot * Cfg::STAGE;
+      const char* zs = ys + Cfg::YBYTES;
+#pragma unroll
+      for (int il = 0; il < 4; ++il) af[il] = tr_frag<YROW>(ys + KK * 32 * YROW + colA[4 * IH + il]);
+      if constexpr (PH == 0 || PH == 2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = tr_frag<ZROW>(zs + KK * 32 * ZROW + colB[j]);
+      }
+    };
+    auto mma = [&](auto ph) {
+      constexpr int PH = decltype(ph)::value, IH = (PH == 1 || PH == 2) ? 1 : 0;
+#pragma unroll
+      for (int il = 0; il < 4; ++il)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 * IH + il][j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(af[il], bf[j], acc[4 * IH + il][j], 0, 0, 0);
+    };
+    pingpong_tiles<0, 0xA>(1, nkl, wm, issue, read, mma, [](int) {});
+  } else {
+    mfma_pipeline<Cfg::S, false, BK / 32, Cfg::YINSTR + Cfg::ZINSTR>(ks_end - ks_begin, acc, stage, frags);
+  }
 
   // native-order slab store: [slice][tile][wave][i*SJ+j][lane] float4
   float4* dst = (float4*)(p.slab + ((size_t)slice * ntile + tile) * Cfg::TILE_FLOATS) +
@@ -170,6 +230,7 @@ hipError_t gemm_tn_dw(const TnParams& p, hipStream_t s) {
       case 0: return launch_tn<TnL0>(p, s);
       case 1: return (p.R % 32) ? hipErrorInvalidValue : launch_tn<TnL1>(p, s);
       case 2: return launch_tn<TnL2>(p, s);
+      case 3: return launch_tn<TnLPP>(p, s);
     }
     return hipErrorInvalidValue;
   }

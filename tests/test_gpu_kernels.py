@@ -51,7 +51,7 @@ def _release():
 
 
 @pytest.fixture(params=[(128, 0, 0), (256, 0, 0), (256, 1, 0), (256, 1, 2), (256, 2, 0), (256, 2, 2),
-                        (256, 3, 3)],
+                        (256, 3, 3), (256, 4, 0), (256, 4, 2), (256, 4, 3)],
                 ids=lambda p: f"t{p[0]}p{p[1]}g{p[2]}")
 def nt_tile(request, lib):
     """Force the NT GEMM tile edge, persistence and persistent grid size (siren_set_option)
@@ -66,7 +66,7 @@ def nt_tile(request, lib):
     lib.siren_set_option(4, 0)
 
 
-@pytest.fixture(params=[0, 1, 2], ids=lambda p: f"p{p}")
+@pytest.fixture(params=[0, 1, 2, 3], ids=lambda p: f"p{p}")
 def tn_pipe(request, lib):
     ok(lib.siren_set_option(3, request.param), lib)
     yield request.param

@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tiles", default="128,256")
-    ap.add_argument("--pipes", default="0,1,2", help="256x256 K-loop variants to time (NT: 0..3, dW: 0..2)")
+    ap.add_argument("--pipes", default="1,4", help="256x256 NT K-loop variants to time (0..4)")
+    ap.add_argument("--tn-pipes", default="0,3", help="256x256 dW K-loop variants to time (0..3)")
     ap.add_argument("--only", default="", help="comma list of case-name prefixes to run")
     ap.add_argument("--staggers", default="", help="SIREN_OPT_NT_STAGGER values to add as "
                     "extra persistent NT cases")
@@ -93,8 +94,9 @@ def main():
             cases[f"fwd_head_{sfx}"] = (tile, pipe, run_fwd_head, flops)
             cases[f"dx_{sfx}"] = (tile, pipe, run_dx, flops)
             cases[f"dx0_{sfx}"] = (tile, pipe, run_dx0, flops)
-            if pipe <= 2:
-                cases[f"dw_{sfx}"] = (tile, pipe, (lambda tl=tile: run_dw(tl)), flops)
+        for pipe in ([int(x) for x in args.tn_pipes.split(",")] if tile == 256 else [0]):
+            sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "")
+            cases[f"dw_{sfx}"] = (tile, pipe, (lambda tl=tile: run_dw(tl)), flops)
     cases["first_fwd"] = (0, 1, run_first, 0.0)
     if args.only:
         pre = tuple(args.only.split(","))
