@@ -196,19 +196,24 @@ enum siren_prof_kind {
 };
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
  * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;
- * SIREN_OPT_NT_PIPE = 256x256 NT GEMM variant: 0 BK 64 one tile per block, 1 BK 64
- * persistent (default), 2 BK 32 4-slot ring persistent, 3 BK 32 3-slot ring persistent,
- * 4 BK 64 persistent with two wave groups in ping-pong;
+ * SIREN_OPT_NT_PIPE = 256x256 NT GEMM variant: -1 per mode (default: 4 for the forward, 1 for
+ * dX), 0 BK 64 one tile per block, 1 BK 64 persistent, 2 BK 32 4-slot ring persistent, 3 BK 32 3-slot ring persistent,
+ * 4 BK 64 persistent with two wave groups in ping-pong, 5 BK 64 persistent with the X operand
+ * prefetched into L2 SIREN_OPT_NT_PF_DIST (1..16, default 2) K-steps ahead;
  * SIREN_OPT_TN_PIPE = 0..3 selects the 256x256 dW K-loop (0: BK 64 double buffer
  * (default), 1: BK 32 4-slot ring, 2: BK 32 5-slot ring, 3: BK 64 ping-pong);
  * SIREN_OPT_NT_GRID = persistent NT grid size (0 = one block per CU; tests use small
  * values so every block walks several tiles);
+ * SIREN_OPT_NT_DIAG = measurement-only NT ablations (results are WRONG while set): bit 0 reads
+ *   the X operand from the first 4 row bands only (L2-resident operand), bit 1 drops the
+ *   epilogue's global stores (values kept live);
  * SIREN_OPT_NT_STAGGER = persistent NT start stagger: block b idles (b % 16) * value units of
  * ~1.7k cycles before its first tile, so that the blocks' epilogue store bursts do not
  * coincide (0 = none; 0..64). */
 enum siren_option {
   SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1, SIREN_OPT_NT_PIPE = 2, SIREN_OPT_TN_PIPE = 3,
-  SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_STAGGER = 5
+  SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_STAGGER = 5, SIREN_OPT_NT_DIAG = 6,
+  SIREN_OPT_NT_PF_DIST = 7
 };
 int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);

@@ -408,13 +408,22 @@ int siren_set_option(int32_t option, int32_t value) {
       return SIREN_OK;
     case SIREN_OPT_NT_PIPE:
     case SIREN_OPT_TN_PIPE:
-      if (value < 0 || value > (option == SIREN_OPT_NT_PIPE ? 4 : 3)) return SIREN_ERR_CONFIG;
+      if (value < (option == SIREN_OPT_NT_PIPE ? -1 : 0) || value > (option == SIREN_OPT_NT_PIPE ? 5 : 3))
+        return SIREN_ERR_CONFIG;
       if (option == SIREN_OPT_NT_PIPE) gemm_nt_set_pipe(value);
       else gemm_tn_set_pipe(value);
       return SIREN_OK;
     case SIREN_OPT_NT_GRID:
       if (value < 0) return SIREN_ERR_CONFIG;
       gemm_nt_set_grid_cap(value);
+      return SIREN_OK;
+    case SIREN_OPT_NT_PF_DIST:
+      if (value < 1 || value > 16) return SIREN_ERR_CONFIG;
+      gemm_nt_set_pf_dist(value);
+      return SIREN_OK;
+    case SIREN_OPT_NT_DIAG:
+      if (value < 0 || value > 3) return SIREN_ERR_CONFIG;
+      gemm_nt_set_diag(value);
       return SIREN_OK;
     case SIREN_OPT_NT_STAGGER:
       if (value < 0 || value > 64) return SIREN_ERR_CONFIG;

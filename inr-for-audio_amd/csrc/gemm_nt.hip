@@ -43,10 +43,13 @@ __device__ __forceinline__ int stage_swz(int r, int c) {
   else return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3);  // H as 2-bit fields of 0x78
 }
 
-template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_, bool PP_ = false>
+template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_, bool PP_ = false, int PF_ = 0>
 struct NtCfg {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, S = S_;
   static constexpr bool PP = PP_;  // ping-pong K-loop (gemm_pipeline.h pingpong_tiles)
+  // L2 prefetch of the X operand p.pf_dist K-steps ahead of the LDS-DMA: one 4-B touch per
+  // 128-B line, PF instructions per wave per stage (BM*BK*2/128 lines over the block)
+  static constexpr int PF = PF_;
   static constexpr int WM = WM_, WN = WN_, NWAVES = WM_ * WN_, THREADS = 64 * NWAVES;
   static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   static constexpr int SM = TM / 16, SN = TN / 16;  // 16x16 MFMA tiles per wave
@@ -59,7 +62,8 @@ struct NtCfg {
   // then (NT_FWD) the whole bias and head weight vectors, staged once per block
   static constexpr int RED = 4 * (WN * BM > 3 * WM * BN ? WN * BM : 3 * WM * BN);
   static constexpr int MAXN = 1024;
-  static constexpr int LDS = RING + RED + 2 * 4 * MAXN;
+  static constexpr int PFLDS = RING + RED + 2 * 4 * MAXN;  // 256-B prefetch landing area
+  static constexpr int LDS = PFLDS + (PF ? 256 : 0);
   static constexpr int XINSTR = XBYTES / 1024 / NWAVES;  // LDS-DMA instructions per wave per stage
   static constexpr int WINSTR = WBYTES / 1024 / NWAVES;
   static_assert(XBYTES % (1024 * NWAVES) == 0 && WBYTES % (1024 * NWAVES) == 0, "staging split");
@@ -74,6 +78,8 @@ using NtLargeR4 = NtCfg<256, 256, 2, 4, 32, 4>;
 using NtLargeR3 = NtCfg<256, 256, 2, 4, 32, 3>;
 // BK 64 double buffer, persistent, two wave groups in ping-pong (SIREN_OPT_NT_PIPE 4)
 using NtLargePP = NtCfg<256, 256, 2, 4, 64, 2, true>;
+// BK 64 double buffer, persistent, X prefetched into L2 ahead of the LDS-DMA (NT_PIPE 5)
+using NtLargePF = NtCfg<256, 256, 2, 4, 64, 2, false, 1>;
 
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
@@ -132,12 +138,27 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     tile_of(ti, m0, n0);
     const char* xs = smem + slot * Cfg::STAGE + wave * Cfg::XINSTR * 1024;
     const char* ws = smem + slot * Cfg::STAGE + Cfg::XBYTES + wave * Cfg::WINSTR * 1024;
-    const h16* xk = p.X + (size_t)m0 * K + kt * BK;
+    const h16* xk = p.X + (size_t)((p.diag & 1) ? (m0 & (4 * BM - 1)) : m0) * K + kt * BK;
     const h16* wk = p.W + (size_t)n0 * K + kt * BK;
 #pragma unroll
     for (int j = 0; j < Cfg::XINSTR; ++j) glds16_asm(xk + xrel[j], lds_addr(xs + j * 1024));
 #pragma unroll
     for (int j = 0; j < Cfg::WINSTR; ++j) glds16_asm(wk + wrel[j], lds_addr(ws + j * 1024));
+    if constexpr (Cfg::PF > 0) {
+      static_assert(Cfg::PF * Cfg::NWAVES * 32 * 128 == BM * ROWB, "one touch per 128-B X line");
+      // K-step pf_dist ahead (always issued -- the counted waits assume PF ops per stage;
+      // past the block's last tile it re-touches this stage)
+      int pt = ti, pk = kt + p.pf_dist;
+      while (pk >= p.K / BK) { pk -= p.K / BK; ++pt; }
+      if (pt >= my_tiles) pt = ti, pk = kt;
+      int pm0, pn0;
+      tile_of(pt, pm0, pn0);
+#pragma unroll
+      for (int j = 0; j < Cfg::PF; ++j) {
+        const int r = (wave * Cfg::PF + j) * 32 + (lane & 31);
+        gpf4_asm(p.X + (size_t)(pm0 + r) * K + pk * BK + (lane >> 5) * 32, lds_addr(smem + Cfg::PFLDS));
+      }
+    }
   };
 
   // ---- fragment read offsets --------------------------------------------------------
@@ -168,6 +189,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // Global traffic goes in 16-B row pieces: column subtiles (2p, 2p+1) are exchanged with
   // swap16_pair, this lane's piece starting at column ncol + 32p + swap16_col(lane).
   float* red = (float*)(smem + Cfg::RING);
+  // 16-B epilogue store; SIREN_OPT_NT_DIAG bit 1 (measurement only) keeps the value live
+  // and drops the store
+  auto st16 = [&](h16* dst, uint4 v) {
+    if (p.diag & 2) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+    else *(uint4*)dst = v;
+  };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
   float* bias_lds = (float*)(smem + Cfg::RING + Cfg::RED);
@@ -250,8 +277,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             if constexpr (HEAD)
               hp[j] += s[0] * hw[i].x + s[1] * hw[i].y + s[2] * hw[i].z + s[3] * hw[i].w;
           }
-          *(uint4*)(p.Y + rowoff + npc + pp * 32) = swap16_pair(ys[0], ys[1]);
-          *(uint4*)(p.C + rowoff + npc + pp * 32) = swap16_pair(cs[0], cs[1]);
+          st16(p.Y + rowoff + npc + pp * 32, swap16_pair(ys[0], ys[1]));
+          st16(p.C + rowoff + npc + pp * 32, swap16_pair(cs[0], cs[1]));
         }
       }
       if constexpr (HEAD) {
@@ -320,7 +347,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
           }
           if constexpr (MODE == NT_DX)
-            *(uint4*)(p.dZ + rowoff + npc + pp * 32) = swap16_pair(dzp[0], dzp[1]);
+            st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
         }
       }
       // partial layout: NT_DX [tm][N]; NT_DX0 [tm][1+in][N] with q=0 -> db0, q=1+j -> dW0[:, j]
@@ -374,7 +401,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       if (ti >= my_tiles) return false;
       int m0, n0;
       tile_of(ti, m0, n0);
-      const h16* src = ((PC & 1) ? p.X + (size_t)m0 * K : p.W + (size_t)n0 * K) + kt * BK;
+      const int xm0 = (p.diag & 1) ? (m0 & (4 * BM - 1)) : m0;
+      const h16* src = ((PC & 1) ? p.X + (size_t)xm0 * K : p.W + (size_t)n0 * K) + kt * BK;
       const char* dst = smem + slot * Cfg::STAGE;
 #pragma unroll
       for (int j = 0; j < 2; ++j) glds16_asm(src + psrc[PC][j], lds_addr(dst + pdst[PC][j]));
@@ -426,7 +454,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     };
     pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(my_tiles, nk, wm, issue, read, mma, tile_end);
   } else {
-    mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
+    mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR + Cfg::PF, SN, SM,
+                        epilogue_stores<Cfg, MODE>(), Cfg::PF>(
         my_tiles, K / BK, acc, stage, frags, pre, epilogue, p.stamps);
   }
 }
@@ -436,6 +465,10 @@ static int g_nt_grid_cap = 0;  // test hook: persistent grid size (0 = one block
 void gemm_nt_set_grid_cap(int cap) { g_nt_grid_cap = cap; }
 static int g_nt_stagger = 0;
 void gemm_nt_set_stagger(int units) { g_nt_stagger = units; }
+static int g_nt_diag = 0;
+static int g_nt_pf_dist = 2;
+void gemm_nt_set_pf_dist(int d) { g_nt_pf_dist = d; }
+void gemm_nt_set_diag(int bits) { g_nt_diag = bits; }
 static unsigned long long* g_nt_stamps = nullptr;
 #ifdef SIREN_NT_STAMPS
 // diagnostic builds only: [grid][256 tiles][4] u64 device buffer, or null to stop recording
@@ -446,6 +479,8 @@ template <class Cfg, int MODE, bool HEAD>
 static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent) {
   NtParams p = p_in;
   p.stagger = persistent ? g_nt_stagger : 0;
+  p.diag = g_nt_diag;
+  p.pf_dist = g_nt_pf_dist;
   p.stamps = g_nt_stamps;
   const int ntiles = (p.M / Cfg::BM) * (p.N / Cfg::BN);
   if (g_num_cus == 0) {
@@ -477,7 +512,7 @@ static hipError_t dispatch_mode(int mode, bool head, const NtParams& p, hipStrea
 // tile per block; 1 = BK 64 persistent (default); 2 = BK 32 4-slot ring persistent;
 // 3 = BK 32 3-slot ring persistent; 4 = BK 64 persistent ping-pong (pingpong_tiles)
 static int g_nt_tile = 0;
-static int g_nt_pipe = 1;
+static int g_nt_pipe = -1;  // -1: per mode (FWD: ping-pong 4, DX / DX0: 1; kernel_bench r03)
 void gemm_nt_set_tile(int tile) { g_nt_tile = tile; }
 void gemm_nt_set_pipe(int v) { g_nt_pipe = v; }
 
@@ -494,11 +529,13 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (mode == NT_DX0 && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
   if (p.tile == 256) {
     if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
-    switch (g_nt_pipe) {
+    const int pipe = g_nt_pipe >= 0 ? g_nt_pipe : (mode == NT_FWD ? 4 : 1);
+    switch (pipe) {
       case 0: return dispatch_mode<NtLarge>(mode, head, p, s, false);
       case 2: return dispatch_mode<NtLargeR4>(mode, head, p, s, true);
       case 3: return dispatch_mode<NtLargeR3>(mode, head, p, s, true);
       case 4: return dispatch_mode<NtLargePP>(mode, head, p, s, true);
+      case 5: return dispatch_mode<NtLargePF>(mode, head, p, s, true);
       default: return dispatch_mode<NtLarge>(mode, head, p, s, true);
     }
   }

@@ -132,7 +132,10 @@ __device__ __forceinline__ void lds_barrier() {
 //   epi(tile)              consumes acc; the ring is NOT available to it (own LDS scratch;
 //                          raw barriers only -- every wave calls epi the same number of times).
 // SLACK = vector-memory instructions every wave's epilogue issues (a lower bound; 0 is always
-// safe).  G = LDS-DMA instructions per wave per stage.
+// safe).  G = vector-memory instructions per wave per stage, the last PF of which are L2
+// prefetches of a LATER stage's operand: a stage's wait lets its own PF prefetches stay in
+// flight, so each prefetch has two K-steps to land (in-order vmcnt), and the LDS-DMA it
+// runs ahead of then hits L2.
 // SIREN_NT_STAMPS (diagnostic builds only, tools/nt_stamps.py): thread 0 of each block
 // records per tile {start, cycles in K-step waits+barriers, end of MFMAs, end of epilogue}
 // with s_memtime into stamps[block][tile][4].
@@ -144,30 +147,31 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 }
 #endif
 
-// s_waitcnt vmcnt(G*y + (relaxed ? SLACK : 0)) for a wave-uniform y in [0, J]
-template <int G, int SLACK, int J>
+// s_waitcnt vmcnt(G*y + PF + (relaxed ? SLACK : 0)) for a wave-uniform y in [0, J]
+// (PF: the stage's own trailing L2-prefetch instructions, which may stay in flight)
+template <int G, int SLACK, int J, int PF = 0>
 __device__ __forceinline__ void wait_stage(int y, bool relaxed) {
   if constexpr (J >= 0) {
     if (y == J) {
-      if (relaxed) wait_vmcnt<G * J + SLACK>();
-      else wait_vmcnt<G * J>();
+      if (relaxed) wait_vmcnt<G * J + PF + SLACK>();
+      else wait_vmcnt<G * J + PF>();
       return;
     }
-    wait_stage<G, SLACK, J - 1>(y, relaxed);
+    wait_stage<G, SLACK, J - 1, PF>(y, relaxed);
   } else {
     wait_vmcnt<0>();
   }
 }
 
-template <int S, int KK, int G, int NA, int NB, int SLACK, class StageFn, class FragFn, class PreFn,
-          class EpiFn>
+template <int S, int KK, int G, int NA, int NB, int SLACK, int PF, class StageFn, class FragFn,
+          class PreFn, class EpiFn>
 __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&acc)[NA][NB],
                                                     StageFn&& stage, FragFn&& frags, PreFn&& pre,
                                                     EpiFn&& epi,
                                                     unsigned long long* stamps = nullptr) {
   static_assert(S >= 2 && S <= 6, "ring depth");
   constexpr int YMAX = (S == 2) ? 1 : S - 2;  // younger stages in flight at a wait
-  static_assert(SLACK >= 0 && G * YMAX + SLACK < 64, "vmcnt immediate");
+  static_assert(SLACK >= 0 && PF >= 0 && PF <= G && G * YMAX + PF + SLACK < 64, "vmcnt immediate");
   const int total = ntiles * nk;
   if (total <= 0) return;
 #ifdef SIREN_NT_STAMPS
@@ -194,7 +198,7 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
   int relax = 0;  // K-steps left whose stage was issued before the last epilogue's stores
   for (int u = 0; u < total; ++u) {
     SIREN_STAMP(st_a = stamp_now(); if (ck == 0) { st_tile = st_a; st_wait = 0; })
-    wait_stage<G, SLACK, YMAX>(issued - (u + 1), relax > 0);
+    wait_stage<G, SLACK, YMAX, PF>(issued - (u + 1), relax > 0);
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     SIREN_STAMP(st_wait += stamp_now() - st_a;)

@@ -57,6 +57,22 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_byte) 
       : "memory");
 }
 
+// L2 prefetch: a 4-B LDS-DMA per lane (one touch per 128-B line) into a dummy 256-B LDS
+// area.  LDS-DMA rather than a load to a VGPR, whose late return would clobber a register
+// the compiler has already reused.  Counted by vmcnt like every other vector-memory op.
+__device__ __forceinline__ void gpf4_asm(const void* gsrc, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte))
+      : "memory");
+}
+
 __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const LDS_AS char*)(p);
 }

@@ -31,6 +31,8 @@ struct NtParams {
   int in_dim;
   const float* gscale;  // NT_DX / NT_DX0: {S, 1/S} -- column partials are multiplied by 1/S
                         // (null = unscaled)
+  int pf_dist;          // NT_PIPE 5: X L2-prefetch distance in K-steps
+  int diag;             // SIREN_OPT_NT_DIAG ablation bits (0 in production)
   int stagger;          // persistent grid: block b idles (b % 16) * stagger * ~1.7k cycles first
   unsigned long long* stamps;  // SIREN_NT_STAMPS diagnostic builds only
 };
@@ -42,6 +44,8 @@ void gemm_tn_set_tile(int tile);
 void gemm_nt_set_pipe(int v);     // 1 = persistent 256x256 (default), 0 = one tile per block
 void gemm_tn_set_pipe(int v);     // 256x256 K-loop variant (TnL0..TnL2)
 void gemm_nt_set_grid_cap(int cap);  // persistent grid size override (0 = #CUs)
+void gemm_nt_set_pf_dist(int d);   // SIREN_OPT_NT_PF_DIST
+void gemm_nt_set_diag(int bits);     // SIREN_OPT_NT_DIAG (measurement-only ablations)
 void gemm_nt_set_stagger(int units); // persistent grid start stagger (see NtParams::stagger)
 struct TnParams {
   const h16* Y;   // [R][Hin]   layer input (A role: dW column index k)

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--only", default="", help="comma list of case-name prefixes to run")
     ap.add_argument("--staggers", default="", help="SIREN_OPT_NT_STAGGER values to add as "
                     "extra persistent NT cases")
+    ap.add_argument("--diags", default="", help="SIREN_OPT_NT_DIAG ablation bits to add as extra "
+                    "NT cases (1: L2-resident X, 2: no epilogue stores, 3: both); timing only")
+    ap.add_argument("--pf-dists", default="2", help="SIREN_OPT_NT_PF_DIST values for NT pipe 5")
     args = ap.parse_args()
     import __graft_entry__ as ge
     ge.build()
@@ -86,18 +89,30 @@ def main():
         return lib.siren_inner_bwd_dw(P(Y), P(dZ), R, H, splits, tile, P(slabs[splits]), s())
 
     cases = {}
+    pfd = {}
     pipes = [int(x) for x in args.pipes.split(",")]
     for tile in tiles:
         for pipe in (pipes if tile == 256 else [0]):
-            sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "")
-            cases[f"fwd_{sfx}"] = (tile, pipe, run_fwd, flops)
-            cases[f"fwd_head_{sfx}"] = (tile, pipe, run_fwd_head, flops)
-            cases[f"dx_{sfx}"] = (tile, pipe, run_dx, flops)
-            cases[f"dx0_{sfx}"] = (tile, pipe, run_dx0, flops)
+            for d in ([int(x) for x in args.pf_dists.split(",")] if pipe == 5 else [0]):
+                sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "") + (f"f{d}" if d else "")
+                for nm, fn in (("fwd", run_fwd), ("fwd_head", run_fwd_head), ("dx", run_dx), ("dx0", run_dx0)):
+                    cases[f"{nm}_{sfx}"] = (tile, pipe, fn, flops)
+                    pfd[f"{nm}_{sfx}"] = d
         for pipe in ([int(x) for x in args.tn_pipes.split(",")] if tile == 256 else [0]):
             sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "")
             cases[f"dw_{sfx}"] = (tile, pipe, (lambda tl=tile: run_dw(tl)), flops)
     cases["first_fwd"] = (0, 1, run_first, 0.0)
+    # library calibration points (hipBLASLt through torch): the same contraction shapes with
+    # no epilogue, fp16 and bf16 operands, fp16/bf16 output
+    Xb, Wb, dZb = X.to(torch.bfloat16), W.to(torch.bfloat16), dZ.to(torch.bfloat16)
+    Yl = torch.empty(R, H, dtype=bf, device=dev)
+    Ylb = torch.empty(R, H, dtype=torch.bfloat16, device=dev)
+    dWl = torch.empty(H, H, dtype=bf, device=dev)
+    dWlb = torch.empty(H, H, dtype=torch.bfloat16, device=dev)
+    cases["lib_nt_f16"] = (0, 1, lambda: torch.mm(X, W.t(), out=Yl), flops)
+    cases["lib_nt_bf16"] = (0, 1, lambda: torch.mm(Xb, Wb.t(), out=Ylb), flops)
+    cases["lib_tn_f16"] = (0, 1, lambda: torch.mm(dZ.t(), X, out=dWl), flops)
+    cases["lib_tn_bf16"] = (0, 1, lambda: torch.mm(dZb.t(), Xb, out=dWlb), flops)
     if args.only:
         pre = tuple(args.only.split(","))
         cases = {k: v for k, v in cases.items() if k.startswith(pre)}
@@ -107,10 +122,30 @@ def main():
             if v and k.endswith("p1") and not k.startswith("dw") and stagger[k] == 0:
                 cases[f"{k}_s{v}"] = c
                 stagger[f"{k}_s{v}"] = v
+    diag = {k: 0 for k in cases}
+    for v in [int(x) for x in args.diags.split(",") if x]:
+        for k, c in list(cases.items()):
+            if k.startswith(("fwd", "dx")) and stagger.get(k, 0) == 0 and diag[k] == 0:
+                cases[f"{k}_d{v}"] = c
+                diag[f"{k}_d{v}"] = v
+                stagger[f"{k}_d{v}"] = 0
     times = {k: [] for k in cases}
     for _ in range(args.rounds):
         for name, (tile, pipe, fn, _) in cases.items():
+            if name.startswith("lib"):
+                fn()
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ev0.record()
+                for _ in range(args.reps):
+                    fn()
+                ev1.record()
+                torch.cuda.synchronize()
+                times[name].append(ev0.elapsed_time(ev1) / args.reps)
+                continue
             lib.siren_set_option(5, stagger[name])
+            lib.siren_set_option(6, diag.get(name, 0))
+            if pfd.get(name, 0):
+                lib.siren_set_option(7, pfd[name])
             lib.siren_set_option(0, tile if not name.startswith("dw") else 0)
             if name.startswith("dw"):
                 lib.siren_set_option(3, pipe)
@@ -126,8 +161,9 @@ def main():
             torch.cuda.synchronize()
             times[name].append(ev0.elapsed_time(ev1) / args.reps)
     lib.siren_set_option(5, 0)
+    lib.siren_set_option(6, 0)
     lib.siren_set_option(0, 0)
-    lib.siren_set_option(2, 1)
+    lib.siren_set_option(2, -1)
     lib.siren_set_option(3, 0)
     out = {}
     for name, (tile, pipe, fn, fl) in cases.items():
