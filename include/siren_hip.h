@@ -26,8 +26,8 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 2
-#define SIREN_MAX_INNER 16  /* max hidden SineLayers (num_sine) */
+#define SIREN_ABI_VERSION 3
+#define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 
 enum siren_status {
@@ -51,9 +51,13 @@ typedef struct siren_opt_state {
   double beta1, beta2, eps;
 } siren_opt_state;
 
-/* ---- one SIREN L x H network (SirenWithSnakeTanh, sine-only; models.py:306-394) --------
- * net.0 = SineLayer(in, H, is_first, omega0); net.1..net.L = SineLayer(H, H, omega);
- * net.{L+1} = Linear(H, 1).  Inner layer i (0-based) is net.{i+1}. */
+/* ---- one L x H network (SirenWithSnakeTanh, models.py:306-394) ------------------------
+ * net.0 = SineLayer(in, H, is_first, omega0); then L inner layers H -> H, each a
+ * SineLayer(H, H, omega) (models.py:114-115), a Linear + Snake(a) (models.py:356-364,
+ * 235-241) or a Linear + Tanh (models.py:366-372), in the reference's order (num_sine
+ * sines, then num_snake Snakes, then num_tanh Tanhs); last: Linear(H, 1).  act[i] says
+ * which (siren_act); a[i] is the Snake's per-channel a [H]. */
+enum siren_act { SIREN_ACT_SINE = 0, SIREN_ACT_SNAKE = 1, SIREN_ACT_TANH = 2 };
 typedef struct siren_net {
   int32_t in_dim, hidden, n_inner, pad0;
   float omega0, omega;
@@ -62,8 +66,10 @@ typedef struct siren_net {
   const float* b[SIREN_MAX_INNER];          /* [H]           */
   const uint16_t* Wh[SIREN_MAX_INNER];      /* [H][H] fp16 shadow of W_i   */
   const uint16_t* WTh[SIREN_MAX_INNER];     /* [H][H] fp16 shadow of W_i^T */
-  const float* w_head;                      /* [H] (net.{L+1}.weight[0])   */
+  const float* w_head;                      /* [H] (last Linear's weight[0]) */
   const float* b_head;                      /* [1]                          */
+  int32_t act[SIREN_MAX_INNER];             /* siren_act of inner layer i   */
+  const float* a[SIREN_MAX_INNER];          /* [H] Snake a (SNAKE layers)   */
 } siren_net;
 
 /* gradient destinations (fp32, accumulated into: zero them, or set zero_grads) */
@@ -73,6 +79,7 @@ typedef struct siren_grads {
   float* w_head; float* b_head;
   float* sse;                               /* [1] sum of squared errors of valid rows */
   float* flat; int64_t flat_len;            /* if flat != NULL and zero_grads: memset   */
+  float* a[SIREN_MAX_INNER];                /* [H] Snake a gradients (SNAKE layers)     */
 } siren_grads;
 
 /* per-micro-batch activations and workspace; sizes from siren_workspace_floats() */
@@ -84,8 +91,9 @@ typedef struct siren_batch {
   int32_t zero_grads;    /* 1: zero `grads.flat` before accumulating         */
   const float* coords;   /* [rows][in]  */
   const float* target;   /* [rows]      */
-  uint16_t* Y[SIREN_MAX_INNER + 1];  /* Y[0..L] fp16 [rows][H]: layer outputs sin(.)  */
-  uint16_t* C[SIREN_MAX_INNER + 1];  /* C[0..L] fp16 [rows][H]: cos(.) of every layer  */
+  uint16_t* Y[SIREN_MAX_INNER + 1];  /* Y[0..L] fp16 [rows][H]: layer outputs          */
+  uint16_t* C[SIREN_MAX_INNER + 1];  /* C[0..L] fp16 [rows][H]: cos(.) of a sine layer,
+                                        dY/dz of a Snake / Tanh layer                 */
   uint16_t* dZ[2];       /* fp16 [rows][H] ping-pong pre-activation gradients x S */
   float* out;            /* [rows] model output                                 */
   float* g;              /* [rows] dLoss/dout                                   */
@@ -98,6 +106,8 @@ typedef struct siren_batch {
   float* col_part2;      /* [rows/128][H]                                       */
   float* red_tmp;        /* [64][H]                                             */
   float* slab;           /* [splits][H][H]                                      */
+  uint16_t* E[SIREN_MAX_INNER + 1];  /* E[i+1] fp16 [rows][H]: dY/da of Snake inner layer
+                                        i (NULL for other layers)                      */
 } siren_batch;
 
 /* Workspace sizing / tiling helpers.  siren_nt_tile: tile edge the NT GEMMs use for
@@ -141,6 +151,13 @@ int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float
 int siren_inner_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, float omega, int32_t rows,
                     int32_t hidden, uint16_t* Y, uint16_t* C, const float* head_w, float* head_part,
                     void* stream);
+/* any inner layer kind: SINE as siren_inner_fwd; SNAKE (models.py:235-241): z = X W^T + b,
+ * Y = z + sin^2(a z)/a, C = 1 + sin(2az), E = (z sin(2az) - sin^2(az)/a)/a; TANH
+ * (models.py:366-372): Y = tanh z, C = 1 - Y^2 (a, E unused) */
+int siren_inner_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, int32_t act,
+                        float omega, const float* a, int32_t rows, int32_t hidden, uint16_t* Y,
+                        uint16_t* C, uint16_t* E, const float* head_w, float* head_part,
+                        void* stream);
 /* run.py:125,168 MSELoss + final Linear bias: out, g = 2(out-y)/n_total, partial sums
  * (gmax_part may be NULL) */
 int siren_head_loss(const float* head_part, int32_t nparts, int32_t rows, const float* b_head,
@@ -150,16 +167,24 @@ int siren_head_loss(const float* head_part, int32_t nparts, int32_t rows, const 
  * from the nparts = rows/256 max |g| partials of siren_head_loss */
 int siren_grad_scale(const float* gmax_part, int32_t nparts, const float* w_head, int32_t hidden,
                      float omega, float* gscale, void* stream);
-/* autograd of Linear(H,1) + last sin: dZ_L (x S), db_L partials, dw_head partials (unscaled);
- * gscale NULL = S 1 */
+/* autograd of Linear(H,1) + the last layer's activation: dZ_L = g w_head omega C (x S),
+ * db_L partials, dw_head partials (unscaled); gscale NULL = S 1.  Snake / Tanh last layer:
+ * omega = 1 (C is their derivative); Snake also passes E and gets da_part (else NULL) */
 int siren_head_bwd(const uint16_t* C, const uint16_t* Y, const float* g, const float* w_head,
                    float omega, int32_t rows, int32_t hidden, const float* gscale, uint16_t* dZ,
-                   float* db_part, float* dwh_part, void* stream);
+                   float* db_part, float* dwh_part, const uint16_t* E, float* da_part, void* stream);
 /* autograd addmm dX + sin/omega backward of the layer below: dZprev = omega*cos*(dZ W)
  * (carries dZ's scale); db partials multiplied by 1/S (gscale NULL = unscaled) */
 int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTh, const uint16_t* Cprev, float omega_prev,
                        int32_t rows, int32_t hidden, const float* gscale, uint16_t* dZprev,
                        float* db_part, void* stream);
+/* the same into a layer below of any kind (act_prev): SINE as above; TANH: dZprev = C (dZ W);
+ * SNAKE: dZprev = D (dZ W) and part [rows/tile][2][H] = partials of db and of da = sum (dZ W) E
+ * (x 1/S) */
+int siren_inner_bwd_dx_act(const uint16_t* dZ, const uint16_t* WTh, const uint16_t* Cprev,
+                           const uint16_t* Eprev, int32_t act_prev, float omega_prev, int32_t rows,
+                           int32_t hidden, const float* gscale, uint16_t* dZprev, float* part,
+                           void* stream);
 /* same into the fp32 first layer (C0 from siren_first_fwd): partials [rows/128][1+in][H]
  * of dZ0 and dZ0*t_j (x 1/S); dZ0 itself is never stored */
 int siren_first_bwd_dx(const uint16_t* dZ1, const uint16_t* WTh1, const uint16_t* C0, const float* t,

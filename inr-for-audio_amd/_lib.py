@@ -13,9 +13,10 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_INNER = 16
 ROW_TILE = 128
+ACT_SINE, ACT_SNAKE, ACT_TANH = 0, 1, 2  # siren_act
 
 _p = ctypes.c_void_p
 _f32p = ctypes.POINTER(ctypes.c_float)
@@ -42,6 +43,7 @@ class SirenNet(ctypes.Structure):
         ("W0", _p), ("b0", _p),
         ("b", _p * MAX_INNER), ("Wh", _p * MAX_INNER), ("WTh", _p * MAX_INNER),
         ("w_head", _p), ("b_head", _p),
+        ("act", _i32 * MAX_INNER), ("a", _p * MAX_INNER),
     ]
 
 
@@ -51,6 +53,7 @@ class SirenGrads(ctypes.Structure):
         ("W", _p * MAX_INNER), ("b", _p * MAX_INNER),
         ("w_head", _p), ("b_head", _p), ("sse", _p),
         ("flat", _p), ("flat_len", _i64),
+        ("a", _p * MAX_INNER),
     ]
 
 
@@ -62,6 +65,7 @@ class SirenBatch(ctypes.Structure):
         ("Y", _p * (MAX_INNER + 1)), ("C", _p * (MAX_INNER + 1)), ("dZ", _p * 2),
         ("out", _p), ("g", _p), ("head_part", _p), ("sse_part", _p), ("gsum_part", _p),
         ("gmax_part", _p), ("gscale", _p), ("col_part", _p), ("col_part2", _p), ("red_tmp", _p), ("slab", _p),
+        ("E", _p * (MAX_INNER + 1)),
     ]
 
 
@@ -86,7 +90,12 @@ _SIGS = {
     "siren_head_loss": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _i32, ctypes.c_double, _p, _p, _p, _p,
                                        _p, _p]),
     "siren_grad_scale": (ctypes.c_int, [_p, _i32, _p, _i32, ctypes.c_float, _p, _p]),
-    "siren_head_bwd": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p]),
+    "siren_inner_fwd_act": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_float, _p, _i32, _i32, _p, _p, _p, _p,
+                                           _p, _p]),
+    "siren_head_bwd": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p, _p,
+                                      _p]),
+    "siren_inner_bwd_dx_act": (ctypes.c_int, [_p, _p, _p, _p, _i32, ctypes.c_float, _i32, _i32, _p, _p, _p,
+                                              _p]),
     "siren_inner_bwd_dx": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p]),
     "siren_first_bwd_dx": (ctypes.c_int, [_p, _p, _p, _p, _i32, ctypes.c_float, _i32, _i32, _p, _p,
                                           _p]),

@@ -57,9 +57,20 @@ int check_net(const siren_net* n) {
   if (!hidden_ok(n->hidden)) return SIREN_ERR_SHAPE;
   if (n->n_inner < 1 || n->n_inner > SIREN_MAX_INNER) return SIREN_ERR_CONFIG;
   if (!n->W0 || !n->b0 || !n->w_head || !n->b_head) return SIREN_ERR_NULL;
-  for (int i = 0; i < n->n_inner; ++i)
+  for (int i = 0; i < n->n_inner; ++i) {
     if (!n->b[i] || !n->Wh[i] || !n->WTh[i]) return SIREN_ERR_NULL;
+    if (n->act[i] < SIREN_ACT_SINE || n->act[i] > SIREN_ACT_TANH) return SIREN_ERR_CONFIG;
+    if (n->act[i] == SIREN_ACT_SNAKE && !n->a[i]) return SIREN_ERR_NULL;
+  }
   return SIREN_OK;
+}
+
+// forward mode of an inner layer kind; omega its epilogue / derivative factor
+int fwd_mode(int act) { return act == SIREN_ACT_SNAKE ? NT_FWD_SNAKE : (act == SIREN_ACT_TANH ? NT_FWD_TANH : NT_FWD); }
+float act_omega(const siren_net* n, int i) { return n->act[i] == SIREN_ACT_SINE ? n->omega : 1.0f; }
+// bound of |dY/dz| of inner layer i (grad_scale headroom): omega, 2 (Snake), 1 (Tanh)
+float act_bound(const siren_net* n, int i) {
+  return n->act[i] == SIREN_ACT_SINE ? n->omega : (n->act[i] == SIREN_ACT_SNAKE ? 2.0f : 1.0f);
 }
 
 int check_batch(const siren_net* n, const siren_batch* b, bool train) {
@@ -70,6 +81,8 @@ int check_batch(const siren_net* n, const siren_batch* b, bool train) {
     return SIREN_ERR_NULL;
   for (int i = 0; i <= n->n_inner; ++i)
     if (!b->Y[i] || !b->C[i]) return SIREN_ERR_NULL;
+  for (int i = 0; i < n->n_inner; ++i)
+    if (n->act[i] == SIREN_ACT_SNAKE && !b->E[i + 1]) return SIREN_ERR_NULL;
   if (train) {
     if (!b->target || !b->dZ[0] || !b->dZ[1] || !b->col_part || !b->col_part2 || !b->red_tmp ||
         !b->slab || !b->gmax_part || !b->gscale)
@@ -94,10 +107,12 @@ hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s) {
     p.bias = n->b[i];
     p.Y = B(b->Y[i + 1]);
     p.C = B(b->C[i + 1]);
+    p.E = B(b->E[i + 1]);
+    p.act_a = n->a[i];
     const bool head = (i == L - 1);
     p.head_w = n->w_head;
     p.head_part = b->head_part;
-    SIREN_PROF(SIREN_PROF_INNER_FWD, s, gemm_nt(NT_FWD, head, p, s));
+    SIREN_PROF(SIREN_PROF_INNER_FWD, s, gemm_nt(fwd_mode(n->act[i]), head, p, s));
   }
   return hipSuccess;
 }
@@ -153,8 +168,10 @@ int siren_forward(const siren_net* net, siren_batch* batch, void* stream) {
 
 static int check_grads(const siren_net* net, const siren_grads* gr) {
   if (!gr || !gr->W0 || !gr->b0 || !gr->w_head || !gr->b_head) return SIREN_ERR_NULL;
-  for (int i = 0; i < net->n_inner; ++i)
+  for (int i = 0; i < net->n_inner; ++i) {
     if (!gr->W[i] || !gr->b[i]) return SIREN_ERR_NULL;
+    if (net->act[i] == SIREN_ACT_SNAKE && !gr->a[i]) return SIREN_ERR_NULL;
+  }
   return SIREN_OK;
 }
 
@@ -163,12 +180,17 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
   const int R = b->rows, H = net->hidden, L = net->n_inner, in = net->in_dim;
   const int ntile = nt_choose_tile(R, H), tntile = tn_choose_tile(R, H, H);
   const int prow = R / ntile;  // partial rows written by the NT_DX / NT_DX0 epilogues
-  SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale(b->gmax_part, (R + 255) / 256, net->w_head, H, net->omega,
-                                            b->gscale, s));
-  SIREN_PROF(SIREN_PROF_HEAD, s, head_bwd(B(b->C[L]), B(b->Y[L]), b->g, net->w_head, net->omega, R, H,
-                                          b->gscale, B(b->dZ[0]), b->col_part, b->col_part2, s));
+  const bool snake_last = net->act[L - 1] == SIREN_ACT_SNAKE;
+  float* da_last = b->col_part + (int64_t)(R / 128) * H;  // second H-wide slab of col_part
+  SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale(b->gmax_part, (R + 255) / 256, net->w_head, H,
+                                            act_bound(net, L - 1), b->gscale, s));
+  SIREN_PROF(SIREN_PROF_HEAD, s, head_bwd(B(b->C[L]), B(b->Y[L]), b->g, net->w_head, act_omega(net, L - 1),
+                                          R, H, b->gscale, B(b->dZ[0]), b->col_part, b->col_part2,
+                                          snake_last ? B(b->E[L]) : nullptr, snake_last ? da_last : nullptr, s));
   SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part2, H, R / 128, H, gr->w_head, 1, 1, b->red_tmp, s));
   SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, R / 128, H, gr->b[L - 1], 1, 1, b->red_tmp, s));
+  if (snake_last)
+    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(da_last, H, R / 128, H, gr->a[L - 1], 1, 1, b->red_tmp, s));
 
   int cur = 0;
   for (int i = L - 1; i >= 0; --i) {
@@ -191,11 +213,17 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
     p.colsum_part = b->col_part;
     p.gscale = b->gscale;
     if (i > 0) {
-      p.omega = net->omega;
+      const bool snake = net->act[i - 1] == SIREN_ACT_SNAKE;
+      p.omega = act_omega(net, i - 1);
       p.Cprev = B(b->C[i]);
+      p.Eprev = B(b->E[i]);
       p.dZ = B(b->dZ[cur ^ 1]);
-      SIREN_PROF(SIREN_PROF_BWD_DX, s, gemm_nt(NT_DX, false, p, s));
-      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, prow, H, gr->b[i - 1], 1, 1, b->red_tmp, s));
+      SIREN_PROF(SIREN_PROF_BWD_DX, s, gemm_nt(snake ? NT_DX_SNAKE : NT_DX, false, p, s));
+      const int64_t rs = (int64_t)(snake ? 2 : 1) * H;
+      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, rs, prow, H, gr->b[i - 1], 1, 1, b->red_tmp, s));
+      if (snake)
+        SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + H, rs, prow, H, gr->a[i - 1], 1, 1,
+                                                    b->red_tmp, s));
       cur ^= 1;
     } else {
       p.omega = net->omega0;
@@ -316,11 +344,46 @@ int siren_grad_scale(const float* gmax_part, int32_t nparts, const float* w_head
 
 int siren_head_bwd(const uint16_t* C, const uint16_t* Y, const float* g, const float* w_head,
                    float omega, int32_t rows, int32_t hidden, const float* gscale, uint16_t* dZ,
-                   float* db_part, float* dwh_part, void* stream) {
+                   float* db_part, float* dwh_part, const uint16_t* E, float* da_part, void* stream) {
   if (!C || !Y || !g || !w_head || !dZ || !db_part || !dwh_part) return SIREN_ERR_NULL;
+  if (E && !da_part) return SIREN_ERR_NULL;
   if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
   return (int)head_bwd(B(C), B(Y), g, w_head, omega, rows, hidden, gscale, B(dZ), db_part, dwh_part,
-                       S(stream));
+                       B(E), da_part, S(stream));
+}
+
+int siren_inner_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, int32_t act,
+                        float omega, const float* a, int32_t rows, int32_t hidden, uint16_t* Y,
+                        uint16_t* C, uint16_t* E, const float* head_w, float* head_part,
+                        void* stream) {
+  if (!X || !Wh || !b || !Y || !C) return SIREN_ERR_NULL;
+  if (act < SIREN_ACT_SINE || act > SIREN_ACT_TANH) return SIREN_ERR_CONFIG;
+  if (act == SIREN_ACT_SNAKE && (!a || !E)) return SIREN_ERR_NULL;
+  if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
+  if (head_w && !head_part) return SIREN_ERR_NULL;
+  NtParams p = {};
+  p.X = B(X); p.W = B(Wh); p.M = rows; p.N = hidden; p.K = hidden;
+  p.tile = nt_choose_tile(rows, hidden);
+  p.omega = omega; p.bias = b; p.Y = B(Y); p.C = B(C); p.E = B(E); p.act_a = a;
+  p.head_w = head_w; p.head_part = head_part;
+  return (int)gemm_nt(fwd_mode(act), head_w != nullptr, p, S(stream));
+}
+
+int siren_inner_bwd_dx_act(const uint16_t* dZ, const uint16_t* WTh, const uint16_t* Cprev,
+                           const uint16_t* Eprev, int32_t act_prev, float omega_prev, int32_t rows,
+                           int32_t hidden, const float* gscale, uint16_t* dZprev, float* part,
+                           void* stream) {
+  if (!dZ || !WTh || !Cprev || !dZprev || !part) return SIREN_ERR_NULL;
+  if (act_prev < SIREN_ACT_SINE || act_prev > SIREN_ACT_TANH) return SIREN_ERR_CONFIG;
+  if (act_prev == SIREN_ACT_SNAKE && !Eprev) return SIREN_ERR_NULL;
+  if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
+  NtParams p = {};
+  p.X = B(dZ); p.W = B(WTh); p.M = rows; p.N = hidden; p.K = hidden;
+  p.tile = nt_choose_tile(rows, hidden);
+  p.omega = act_prev == SIREN_ACT_SINE ? omega_prev : 1.0f;
+  p.Cprev = B(Cprev); p.Eprev = B(Eprev); p.dZ = B(dZprev); p.colsum_part = part;
+  p.gscale = gscale;
+  return (int)gemm_nt(act_prev == SIREN_ACT_SNAKE ? NT_DX_SNAKE : NT_DX, false, p, S(stream));
 }
 
 int siren_inner_bwd_dx(const uint16_t* dZ, const uint16_t* WTh, const uint16_t* Cprev, float omega_prev,

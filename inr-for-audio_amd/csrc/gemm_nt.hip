@@ -7,6 +7,10 @@
 //            optional HEAD: per-row partial of sum_n Y[m][n]*w_head[n]      -- models.py:374-381
 //   NT_DX  : dz = (acc * Cprev[m][n]) * omega_prev  (h16 out) + column partial sums (db)
 //            = autograd of sin(omega*linear) for the layer below            -- models.py:114-115
+//   NT_FWD_SNAKE : z = acc + b;  Y = z + sin^2(a z)/a, C = 1 + sin(2az) (dY/dz),
+//            E = (z sin(2az) - sin^2(az)/a)/a (dY/da)                      -- models.py:235-241
+//   NT_FWD_TANH  : z = acc + b;  Y = tanh z, C = 1 - Y^2                    -- models.py:366-372
+//   NT_DX_SNAKE  : dz = acc * D (Cprev) + column partials of dz (db) and acc * E (da)
 //   NT_DX0 : same, into the fp32 first layer (Cprev = its cos from first_fwd): only the
 //            column partial sums of dz and dz*t_j (db0, dW0) are written; dZ0 never
 //            reaches HBM.
@@ -63,12 +67,14 @@ struct NtCfg {
   static constexpr int RED = 4 * (WN * BM > 3 * WM * BN ? WN * BM : 3 * WM * BN);
   static constexpr int MAXN = 1024;
   static constexpr int PFLDS = RING + RED + 2 * 4 * MAXN;  // 256-B prefetch landing area
-  static constexpr int LDS = PFLDS + (PF ? 256 : 0);
+  static constexpr int ALDS = PFLDS + (PF ? 256 : 0);      // NT_FWD_SNAKE: a
+  static constexpr int LDS = ALDS;
+  static constexpr int LDS_SNAKE = ALDS + 4 * MAXN;
   static constexpr int XINSTR = XBYTES / 1024 / NWAVES;  // LDS-DMA instructions per wave per stage
   static constexpr int WINSTR = WBYTES / 1024 / NWAVES;
   static_assert(XBYTES % (1024 * NWAVES) == 0 && WBYTES % (1024 * NWAVES) == 0, "staging split");
   static_assert(SN % 2 == 0, "16-B row pieces pair adjacent column subtiles");
-  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(LDS_SNAKE <= 160 * 1024, "LDS");
 };
 using NtSmall = NtCfg<128, 128, 2, 2, 64, 2>;
 // 256x256 variants (siren_set_option SIREN_OPT_NT_PIPE): BK 64 double buffer (one tile per
@@ -84,14 +90,17 @@ using NtLargePF = NtCfg<256, 256, 2, 4, 64, 2, false, 1>;
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
 constexpr int epilogue_stores() {
-  return MODE == NT_FWD ? Cfg::SM * Cfg::SN : (MODE == NT_DX ? Cfg::SM * Cfg::SN / 2 : 0);
+  return (MODE == NT_FWD || MODE == NT_FWD_TANH) ? Cfg::SM * Cfg::SN
+         : MODE == NT_FWD_SNAKE                 ? 3 * Cfg::SM * Cfg::SN / 2
+         : (MODE == NT_DX || MODE == NT_DX_SNAKE) ? Cfg::SM * Cfg::SN / 2
+                                                  : 0;
 }
 
 template <class Cfg, int MODE, bool HEAD>
 __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, BK = Cfg::BK, WN = Cfg::WN;
   constexpr int TM = Cfg::TM, TN = Cfg::TN, SM = Cfg::SM, SN = Cfg::SN;
-  __shared__ __attribute__((aligned(16))) char smem[Cfg::LDS];
+  __shared__ __attribute__((aligned(16))) char smem[MODE == NT_FWD_SNAKE ? Cfg::LDS_SNAKE : Cfg::LDS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -199,17 +208,19 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
   float* bias_lds = (float*)(smem + Cfg::RING + Cfg::RED);
   float* hw_lds = bias_lds + Cfg::MAXN;
-  if constexpr (MODE == NT_FWD) {
+  float* a_lds = (float*)(smem + Cfg::ALDS);  // Snake: a
+  if constexpr (nt_is_fwd(MODE)) {
     for (int c = tid * 4; c < N; c += Cfg::THREADS * 4) {
       *(float4*)(bias_lds + c) = *(const float4*)(p.bias + c);
       if constexpr (HEAD) *(float4*)(hw_lds + c) = *(const float4*)(p.head_w + c);
+      if constexpr (MODE == NT_FWD_SNAKE) *(float4*)(a_lds + c) = *(const float4*)(p.act_a + c);
     }
     // visible to other waves after the pipeline's first barrier
   }
   // dZ carries the backward storage scale S; the fp32 column partials leave unscaled
-  const float inv_scale = (MODE != NT_FWD && p.gscale) ? p.gscale[1] : 1.0f;
+  const float inv_scale = (!nt_is_fwd(MODE) && p.gscale) ? p.gscale[1] : 1.0f;
   // NT_DX / NT_DX0 epilogue operands loaded by `pre` (before the next tile's early prefetch)
-  constexpr int PRE_J = (MODE == NT_FWD) ? 0 : (MODE == NT_DX ? SM : SM / 2);
+  constexpr int PRE_J = nt_is_fwd(MODE) ? 0 : (MODE == NT_DX ? SM : SM / 2);
   uint4 cp_in[PRE_J > 0 ? PRE_J : 1][SN / 2];
   float t_in[SM][2];
   auto pre = [&](int ti) {
@@ -217,7 +228,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     tile_of(ti, m0, n0);
     const int npc = n0 + wn * TN + swap16_col(lane);
     const int mrow0 = m0 + wm * TM + (lane & 15);
-    if constexpr (MODE != NT_FWD) {
+    if constexpr (!nt_is_fwd(MODE)) {
 #pragma unroll
       for (int j = 0; j < PRE_J; ++j)
 #pragma unroll
@@ -240,9 +251,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     const int npc = n0 + wn * TN + swap16_col(lane);      // swapped layout: this lane's piece
     const int mrow0 = m0 + wm * TM + (lane & 15);
 
-    if constexpr (MODE == NT_FWD) {
+    if constexpr (nt_is_fwd(MODE)) {
       const int nq = n0 + wn * TN + 4 * (lane >> 4);     // natural layout: this lane's columns
-      const float xs = p.omega * kInv2Pi;
+      const float xs = (MODE == NT_FWD) ? p.omega * kInv2Pi : 1.0f;
       float4 bias[SN], hw[SN];
 #pragma unroll
       for (int i = 0; i < SN; ++i) {
@@ -258,27 +269,52 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
-          uint2 ys[2], cs[2];
+          uint2 ys[2], cs[2], es[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int i = 2 * pp + h;
             const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
-            float s[4], c[4];
+            float s[4], c[4], e[4];
+            if constexpr (MODE == NT_FWD) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
-              // hardware sin/cos inside their reduced domain for any magnitude.
-              const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
-              s[r] = __builtin_amdgcn_sinf(x);
-              c[r] = __builtin_amdgcn_cosf(x);
+              for (int r = 0; r < 4; ++r) {
+                // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
+                // hardware sin/cos inside their reduced domain for any magnitude.
+                const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
+                s[r] = __builtin_amdgcn_sinf(x);
+                c[r] = __builtin_amdgcn_cosf(x);
+              }
+            } else if constexpr (MODE == NT_FWD_SNAKE) {
+              const float4 a4 = *(const float4*)(a_lds + nq + i * 16);
+              const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float z = acc[i][j][r] + bb[r];
+                const float ia = 1.0f / av[r];
+                const float x = __builtin_amdgcn_fractf((z * av[r]) * kInv2Pi);  // a z in revolutions
+                const float sn = __builtin_amdgcn_sinf(x), cn = __builtin_amdgcn_cosf(x);
+                const float s2 = sn * sn, sc2 = 2.0f * sn * cn;
+                s[r] = z + s2 * ia;                    // models.py:241
+                c[r] = 1.0f + sc2;                     // dY/dz
+                e[r] = (z * sc2 - s2 * ia) * ia;       // dY/da
+              }
+            } else {  // NT_FWD_TANH
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float y = tanhf(acc[i][j][r] + bb[r]);
+                s[r] = y;
+                c[r] = 1.0f - y * y;
+              }
             }
             ys[h] = as_u2(pack4(s[0], s[1], s[2], s[3]));
             cs[h] = as_u2(pack4(c[0], c[1], c[2], c[3]));
+            if constexpr (MODE == NT_FWD_SNAKE) es[h] = as_u2(pack4(e[0], e[1], e[2], e[3]));
             if constexpr (HEAD)
               hp[j] += s[0] * hw[i].x + s[1] * hw[i].y + s[2] * hw[i].z + s[3] * hw[i].w;
           }
           st16(p.Y + rowoff + npc + pp * 32, swap16_pair(ys[0], ys[1]));
           st16(p.C + rowoff + npc + pp * 32, swap16_pair(cs[0], cs[1]));
+          if constexpr (MODE == NT_FWD_SNAKE) st16(p.E + rowoff + npc + pp * 32, swap16_pair(es[0], es[1]));
         }
       }
       if constexpr (HEAD) {
@@ -304,7 +340,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       // column sums over this tile's BM rows (db / dW0 partials): per lane over its SM row
       // tiles, over the 16 row-lanes by DPP, then over the WM row waves through LDS.
       const int in_dim = (MODE == NT_DX0) ? p.in_dim : 0;
-      const int nred = 1 + in_dim;
+      const int nred = (MODE == NT_DX_SNAKE) ? 2 : 1 + in_dim;
       float cs[3][SN][4];
 #pragma unroll
       for (int q = 0; q < 3; ++q)
@@ -329,6 +365,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           const uint4 cpv = (j < PRE_J) ? cp_in[j < PRE_J ? j : 0][pp]
                                         : *(const uint4*)(p.Cprev + rowoff + npc + pp * 32);
           unswap16_pair(cpv, cpu[0], cpu[1]);
+          uint2 epu[2];
+          if constexpr (MODE == NT_DX_SNAKE)
+            unswap16_pair(*(const uint4*)(p.Eprev + rowoff + npc + pp * 32), epu[0], epu[1]);
           uint2 dzp[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
@@ -343,14 +382,16 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                 cs[1][i][r] += dz[r] * t0;
                 cs[2][i][r] += dz[r] * t1;
               }
+              if constexpr (MODE == NT_DX_SNAKE) cs[1][i][r] += acc[i][j][r] * (float)as_h4(epu[h])[r];
             }
             dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
           }
-          if constexpr (MODE == NT_DX)
+          if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE)
             st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
         }
       }
-      // partial layout: NT_DX [tm][N]; NT_DX0 [tm][1+in][N] with q=0 -> db0, q=1+j -> dW0[:, j]
+      // partial layout: NT_DX [tm][N]; NT_DX0 [tm][1+in][N] with q=0 -> db0, q=1+j -> dW0[:, j];
+      // NT_DX_SNAKE [tm][2][N] with q=0 -> db, q=1 -> da
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         if (q >= nred) break;
@@ -508,6 +549,21 @@ static hipError_t dispatch_mode(int mode, bool head, const NtParams& p, hipStrea
   return hipErrorInvalidValue;
 }
 
+// Snake / Tanh layers: the default persistent K-loop (or the 128x128 tile)
+template <class Cfg>
+static hipError_t dispatch_act(int mode, bool head, const NtParams& p, hipStream_t s, bool persistent) {
+  switch (mode) {
+    case NT_FWD_SNAKE:
+      return head ? launch_nt<Cfg, NT_FWD_SNAKE, true>(p, s, persistent)
+                  : launch_nt<Cfg, NT_FWD_SNAKE, false>(p, s, persistent);
+    case NT_FWD_TANH:
+      return head ? launch_nt<Cfg, NT_FWD_TANH, true>(p, s, persistent)
+                  : launch_nt<Cfg, NT_FWD_TANH, false>(p, s, persistent);
+    case NT_DX_SNAKE: return launch_nt<Cfg, NT_DX_SNAKE, false>(p, s, persistent);
+  }
+  return hipErrorInvalidValue;
+}
+
 // tile override for A/B measurement: 0 = auto, 128 or 256; pipe (256x256): 0 = BK 64, one
 // tile per block; 1 = BK 64 persistent (default); 2 = BK 32 4-slot ring persistent;
 // 3 = BK 32 3-slot ring persistent; 4 = BK 64 persistent ping-pong (pingpong_tiles)
@@ -527,6 +583,16 @@ int nt_choose_tile(int M, int N) {
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (p.M % NtSmall::BM || p.N % NtSmall::BN || p.K % NtSmall::BK || p.M <= 0 || p.N > NtSmall::MAXN) return hipErrorInvalidValue;
   if (mode == NT_DX0 && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
+  if (mode >= NT_FWD_SNAKE) {
+    if ((mode == NT_FWD_SNAKE && (!p.act_a || !p.E)) || (mode == NT_DX_SNAKE && !p.Eprev))
+      return hipErrorInvalidValue;
+    if (p.tile == 256) {
+      if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
+      return dispatch_act<NtLarge>(mode, head, p, s, true);
+    }
+    if (p.tile != 128) return hipErrorInvalidValue;
+    return dispatch_act<NtSmall>(mode, head, p, s, false);
+  }
   if (p.tile == 256) {
     if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
     const int pipe = g_nt_pipe >= 0 ? g_nt_pipe : (mode == NT_FWD ? 4 : 1);

@@ -8,7 +8,10 @@ namespace siren {
 
 typedef _Float16 h16;  // activation / weight-shadow / gradient storage (fp16)
 
-enum NtMode { NT_FWD = 0, NT_DX = 1, NT_DX0 = 2 };
+// NT_FWD_SNAKE / NT_FWD_TANH: Linear + Snake / Tanh forward epilogues; NT_DX_SNAKE: dX into
+// a Snake layer (derivative D and d/da E of the layer below), SURVEY §8 f3
+enum NtMode { NT_FWD = 0, NT_DX = 1, NT_DX0 = 2, NT_FWD_SNAKE = 3, NT_FWD_TANH = 4, NT_DX_SNAKE = 5 };
+constexpr bool nt_is_fwd(int m) { return m == NT_FWD || m == NT_FWD_SNAKE || m == NT_FWD_TANH; }
 
 struct NtParams {
   const h16* X;  // [M][K]
@@ -19,13 +22,16 @@ struct NtParams {
   // NT_FWD
   const float* bias;    // [N]
   h16* Y;              // [M][N]
-  h16* C;              // [M][N]
+  h16* C;              // [M][N]  sine: cos; Snake: dY/dz = 1 + sin(2az); Tanh: 1 - y^2
+  h16* E;              // [M][N]  Snake only: dY/da = (z sin(2az) - sin^2(az)/a) / a
+  const float* act_a;  // [N]     Snake only: a (per output column)
   const float* head_w;  // [N]          (HEAD only)
   float* head_part;     // [N/128][M]   (HEAD only)
   // NT_DX / NT_DX0
-  const h16* Cprev;    // [M][N]  cos of the layer below (NT_DX)
+  const h16* Cprev;    // [M][N]  cos of the layer below (NT_DX); D of a Snake / 1-y^2 of a Tanh
+  const h16* Eprev;    // [M][N]  NT_DX_SNAKE: E of the Snake layer below
   h16* dZ;             // [M][N]  (NT_DX)
-  float* colsum_part;   // NT_DX: [M/128][N];  NT_DX0: [M/128][1+in][N]
+  float* colsum_part;   // NT_DX: [M/128][N];  NT_DX0: [M/128][1+in][N];  NT_DX_SNAKE: [M/128][2][N]
   // NT_DX0 (Cprev = cos of the first layer)
   const float* t;       // [M][in]
   int in_dim;
@@ -74,9 +80,10 @@ hipError_t gmax_partials(const float* g, int R, float* gmax_part, hipStream_t s)
 // gscale[0] = S (dZ storage scale), gscale[1] = 1/S; from (R+255)/256 max|g| partials
 hipError_t grad_scale(const float* gmax_part, int nparts, const float* w_head, int H, float omega,
                       float* gscale, hipStream_t s);
+// E != null (Snake last layer): da_part[R/128][H] = partial sums of g*w_head*E
 hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_head, float omega,
                     int R, int H, const float* gscale, h16* dZ, float* db_part, float* dwh_part,
-                    hipStream_t s);
+                    const h16* E, float* da_part, hipStream_t s);
 // out[c*out_stride] (+)= sum_r part[r*row_stride + c]; tmp holds >= 64*ncols floats
 hipError_t col_reduce(const float* part, int64_t row_stride, int nrows, int ncols, float* out,
                       int out_stride, int accumulate, float* tmp, hipStream_t s);

@@ -43,10 +43,14 @@ class NetSpec:
     n_inner: int
     omega0: float
     omega: float
+    acts: tuple = ()   # siren_act per inner layer (empty: all sine)
+
+    def act(self, i: int) -> int:
+        return self.acts[i] if self.acts else _lib.ACT_SINE
 
 
 def net_spec(model) -> NetSpec:
-    """Validate that `model` is the sine-only SirenWithSnakeTanh the HIP path implements."""
+    """Validate that `model` is a SirenWithSnakeTanh configuration the HIP path implements."""
     spec = getattr(model, "hip_spec", None)
     if spec is None:
         raise TypeError("expected inr_for_audio_amd.models.SirenWithSnakeTanh")
@@ -88,6 +92,8 @@ class Workspace:
         self.rows = R
         self.Y = [e(R, H, dtype=h) for _ in range(L + 1)]
         self.C = [e(R, H, dtype=h) for _ in range(L + 1)]
+        # dY/da of Snake layers (E[i+1] for inner layer i)
+        self.E = [None] + [e(R, H, dtype=h) if spec.act(i) == _lib.ACT_SNAKE else None for i in range(L)]
         self.out = e(R)
         self.g = torch.zeros(R, dtype=f32, device=device)
         self.head_part = e(H // 128, R)
@@ -100,7 +106,7 @@ class Workspace:
         if train:
             self.splits = int(splits or lib.siren_default_splits(R, H))
             self.dZ = [e(R, H, dtype=h) for _ in range(2)]
-            self.col_part = e(R // 128, 1 + spec.in_dim, H)
+            self.col_part = e(R // 128, max(1 + spec.in_dim, 2), H)
             self.col_part2 = e(R // 128, H)
             self.red_tmp = e(64, H)
             self.slab = e(int(lib.siren_slab_floats(H, self.splits)))
@@ -119,6 +125,8 @@ class Workspace:
             b.Y[i] = ptr(y)
         for i, c in enumerate(self.C):
             b.C[i] = ptr(c)
+        for i, x in enumerate(self.E):
+            b.E[i] = ptr(x)
         b.dZ[0], b.dZ[1] = ptr(self.dZ[0]), ptr(self.dZ[1])
         b.out, b.g, b.head_part = ptr(self.out), ptr(self.g), ptr(self.head_part)
         b.sse_part, b.gsum_part = ptr(self.sse_part), ptr(self.gsum_part)
@@ -128,25 +136,31 @@ class Workspace:
         return b
 
 
-def make_net(spec: NetSpec, W0, b0, bs, Whs, WThs, w_head, b_head) -> SirenNet:
+def make_net(spec: NetSpec, W0, b0, bs, Whs, WThs, w_head, b_head, snake_a=None) -> SirenNet:
     n = SirenNet()
     n.in_dim, n.hidden, n.n_inner = spec.in_dim, spec.hidden, spec.n_inner
     n.omega0, n.omega = spec.omega0, spec.omega
     n.W0, n.b0 = ptr(W0), ptr(b0)
     for i in range(spec.n_inner):
         n.b[i], n.Wh[i], n.WTh[i] = ptr(bs[i]), ptr(Whs[i]), ptr(WThs[i])
+        n.act[i] = spec.act(i)
+        if snake_a is not None and snake_a[i] is not None:
+            n.a[i] = ptr(snake_a[i])
     n.w_head, n.b_head = ptr(w_head), ptr(b_head)
     return n
 
 
-def make_grads(spec: NetSpec, layout: ParamLayout, gflat: torch.Tensor) -> SirenGrads:
+def make_grads(spec: NetSpec, layout: ParamLayout, gflat: torch.Tensor, ix: dict) -> SirenGrads:
+    """Gradient destinations: views of `gflat` at the positions of model.param_index()."""
     g = SirenGrads()
     v = lambda i: layout.view(gflat, i)  # noqa: E731
     L = spec.n_inner
-    g.W0, g.b0 = ptr(v(0)), ptr(v(1))
+    g.W0, g.b0 = ptr(v(ix["W0"])), ptr(v(ix["b0"]))
     for i in range(L):
-        g.W[i], g.b[i] = ptr(v(2 + 2 * i)), ptr(v(3 + 2 * i))
-    g.w_head, g.b_head = ptr(v(2 + 2 * L)), ptr(v(3 + 2 * L))
+        g.W[i], g.b[i] = ptr(v(ix["W"][i])), ptr(v(ix["b"][i]))
+        if ix["a"][i] is not None:
+            g.a[i] = ptr(v(ix["a"][i]))
+    g.w_head, g.b_head = ptr(v(ix["wh"])), ptr(v(ix["bh"]))
     g.sse = gflat.data_ptr() + 4 * layout.sse_offset
     g.flat, g.flat_len = ptr(gflat), layout.flat_len
     return g
@@ -203,13 +217,14 @@ class SirenEngine:
         self.exp_avg_sq = torch.zeros_like(self.params)
 
         L, H = spec.n_inner, spec.hidden
+        self.ix = ix = model.param_index()
         pv = lambda i: lay.view(self.params, i)  # noqa: E731
-        self.W = [pv(2 + 2 * i) for i in range(L)]
+        self.W = [pv(k) for k in ix["W"]]
         self.Wh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
         self.WTh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
-        self.net = make_net(spec, pv(0), pv(1), [pv(3 + 2 * i) for i in range(L)], self.Wh, self.WTh,
-                            pv(2 + 2 * L), pv(3 + 2 * L))
-        self.grad_struct = make_grads(spec, lay, self.grads)
+        self.net = make_net(spec, pv(ix["W0"]), pv(ix["b0"]), [pv(k) for k in ix["b"]], self.Wh, self.WTh,
+                            pv(ix["wh"]), pv(ix["bh"]), [None if k is None else pv(k) for k in ix["a"]])
+        self.grad_struct = make_grads(spec, lay, self.grads, ix)
         self._Wp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.W])
         self._Whp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.Wh])
         self._WThp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.WTh])

@@ -51,24 +51,34 @@ class SineLayer(nn.Module):
 
 
 class Snake(nn.Module):
-    """Parameter-compatible Snake (models.py:185-241): y = x + sin^2(a x)/a.  The fused
-    Snake epilogue is a later row of the hot-path table; it has no
-    kernel yet, so forward raises."""
+    """Snake activation y = x + sin^2(a x)/a with per-channel trainable a (models.py:185-241).
+
+    Same parameter, init and RNG use as the reference: a = ones * a, or, for a=None, one
+    Exponential(0.1) rsample per channel (models.py:224-229).  `trainable` is stored as the
+    reference does (the `requiresGrad` attribute, models.py:231), i.e. a always trains.
+    Inside SirenWithSnakeTanh the Linear + Snake pair runs as one fused HIP GEMM epilogue
+    (gemm_nt.hip NT_FWD_SNAKE / NT_DX_SNAKE); a lone Snake has no kernel."""
 
     def __init__(self, in_features, a=None, trainable=True):
         super().__init__()
         self.in_features = in_features if isinstance(in_features, list) else [in_features]
-        initial_a = torch.ones(self.in_features) * (a if a is not None else 1.0)
-        self.a = nn.Parameter(initial_a)
-        self.a.requires_grad = trainable
+        if a is not None:
+            self.a = nn.Parameter(torch.ones(self.in_features) * a)
+        else:
+            m = torch.distributions.exponential.Exponential(torch.tensor([0.1]))
+            self.a = nn.Parameter((m.rsample(self.in_features)).squeeze())
+        self.a.requiresGrad = trainable
 
     def forward(self, x):
-        raise NotImplementedError("Snake epilogue not implemented on the HIP path yet (SURVEY §8 f3)")
+        raise NotImplementedError("a lone Snake has no HIP kernel: wrap it in SirenWithSnakeTanh "
+                                  "(fused Linear + Snake epilogue)")
 
 
 class SirenWithSnakeTanh(nn.Module):
     """MLP with sine / Snake / Tanh activations -- models.py:306-394.  The HIP path covers
-    the SIREN configuration (first SineLayer, num_sine hidden SineLayers, final Linear)."""
+    a first SineLayer, then num_sine SineLayers, num_snake Linear+Snake and num_tanh
+    Linear+Tanh hidden layers, and the final Linear (first_linear=False, last_linear=True,
+    the reference train()'s defaults)."""
 
     def __init__(self, in_features, out_features, hidden_features, num_sine, num_snake, num_tanh,
                  first_linear=False, last_linear=True, first_omega_0=30, hidden_omega_0=30.,
@@ -108,23 +118,51 @@ class SirenWithSnakeTanh(nn.Module):
     def hip_spec(self):
         """NetSpec of the fused path; raises for configurations it does not cover."""
         from .engine import NetSpec
-        if self.first_linear or self.num_snake or self.num_tanh or not self.last_linear:
+        if self.first_linear or not self.last_linear:
             raise NotImplementedError(
-                "HIP path covers the SIREN configuration only (first_linear=False, num_snake=0, "
-                "num_tanh=0, last_linear=True); Snake/Tanh epilogues are SURVEY §8 f3")
+                "HIP path: first_linear=False and last_linear=True (a first Linear+Snake or a "
+                "final SineLayer has no fused kernel)")
         if self.out_features != 1:
             raise NotImplementedError("HIP path: out_features must be 1 (run.py:95,112)")
-        if self.num_sine < 1:
-            raise NotImplementedError("HIP path: num_sine must be >= 1")
+        n_inner = self.num_sine + self.num_snake + self.num_tanh
+        if n_inner < 1:
+            raise NotImplementedError("HIP path: at least one hidden layer (num_sine + num_snake + "
+                                      "num_tanh >= 1)")
         if self.in_features not in (1, 2):
             raise NotImplementedError("HIP path: in_features must be 1 or 2")
         H = self.hidden_features
         if H % 128 or H > 1024 or 256 % (H // 4):
             raise NotImplementedError(f"HIP path: hidden_features must be 128/256/512/1024, got {H}")
-        if self.num_sine > _lib.MAX_INNER:
-            raise NotImplementedError(f"HIP path: num_sine <= {_lib.MAX_INNER}")
-        return NetSpec(self.in_features, H, self.num_sine, float(self.first_omega_0),
-                       float(self.hidden_omega_0))
+        if n_inner > _lib.MAX_INNER:
+            raise NotImplementedError(f"HIP path: num_sine + num_snake + num_tanh <= {_lib.MAX_INNER}")
+        acts = (_lib.ACT_SINE,) * self.num_sine + (_lib.ACT_SNAKE,) * self.num_snake + \
+            (_lib.ACT_TANH,) * self.num_tanh
+        return NetSpec(self.in_features, H, n_inner, float(self.first_omega_0),
+                       float(self.hidden_omega_0), acts)
+
+    def param_index(self):
+        """Positions in named_parameters() order (== state_dict order == Adam's state index)
+        of every tensor the fused path binds: {'W0', 'b0', 'W': [..], 'b': [..], 'a': [.. or
+        None], 'wh', 'bh'} -- SineLayer: net.{i}.linear.{weight,bias}; Linear+Snake:
+        net.{i}.{weight,bias} + net.{i+1}.a; Linear+Tanh: net.{i}.{weight,bias}."""
+        names = [n for n, _ in self.named_parameters()]
+        pos = {n: k for k, n in enumerate(names)}
+        idx = {"W0": pos["net.0.linear.weight"], "b0": pos["net.0.linear.bias"], "W": [], "b": [], "a": []}
+        mods = list(self.net)
+        j = 1
+        for _ in range(self.num_sine):
+            idx["W"].append(pos[f"net.{j}.linear.weight"])
+            idx["b"].append(pos[f"net.{j}.linear.bias"])
+            idx["a"].append(None)
+            j += 1
+        for kind in ["snake"] * self.num_snake + ["tanh"] * self.num_tanh:
+            idx["W"].append(pos[f"net.{j}.weight"])
+            idx["b"].append(pos[f"net.{j}.bias"])
+            idx["a"].append(pos[f"net.{j + 1}.a"] if kind == "snake" else None)
+            j += 2
+        assert isinstance(mods[j], nn.Linear), "last layer must be the final Linear"
+        idx["wh"], idx["bh"] = pos[f"net.{j}.weight"], pos[f"net.{j}.bias"]
+        return idx
 
     def forward(self, coords):
         """(1, N, in) or (N, in) CUDA coords -> (..., N, 1) fp32 output, differentiable in the
@@ -134,7 +172,8 @@ class SirenWithSnakeTanh(nn.Module):
         spec = self.hip_spec()
         lead = coords.shape[:-1]
         params = [p for _, p in self.named_parameters()]
-        out = _SirenFunction.apply(spec, coords.reshape(-1, spec.in_dim).detach(), *params)
+        out = _SirenFunction.apply((spec, self.param_index()), coords.reshape(-1, spec.in_dim).detach(),
+                                   *params)
         return out.reshape(*lead, 1)
 
 
@@ -142,35 +181,36 @@ class _SirenFunction(torch.autograd.Function):
     """HIP forward/backward of the whole SIREN for an arbitrary upstream gradient."""
 
     @staticmethod
-    def forward(ctx, spec, coords, *params):
+    def forward(ctx, spec_idx, coords, *params):
         from .engine import ROW_TILE, STORE16, Workspace, cast_shadows, make_net, round_up
+        spec, ix = spec_idx
         dev = coords.device
         lib = _lib.load()
         L, H = spec.n_inner, spec.hidden
         n = coords.shape[0]
         rows = round_up(max(n, 1), ROW_TILE)
         p = [t.detach().contiguous().float() for t in params]
-        W = [p[2 + 2 * i] for i in range(L)]
+        W = [p[k] for k in ix["W"]]
         Wh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
         WTh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
         s = torch.cuda.current_stream(dev).cuda_stream
         cast_shadows(spec, W, Wh, WTh, s)
-        net = make_net(spec, p[0], p[1], [p[3 + 2 * i] for i in range(L)], Wh, WTh, p[2 + 2 * L],
-                       p[3 + 2 * L])
+        net = make_net(spec, p[ix["W0"]], p[ix["b0"]], [p[k] for k in ix["b"]], Wh, WTh, p[ix["wh"]],
+                       p[ix["bh"]], [None if k is None else p[k] for k in ix["a"]])
         ws = Workspace(spec, rows, dev, train=True)
         xc = torch.zeros(rows, spec.in_dim, dtype=torch.float32, device=dev)
         xc[:n] = coords.float()
         tgt = torch.zeros(rows, dtype=torch.float32, device=dev)
         b = ws.batch(xc, tgt, n, float(n))
         _lib.check(lib.siren_forward(ctypes.byref(net), ctypes.byref(b), s), "siren_forward")
-        ctx.keep = (spec, net, ws, xc, tgt, p, Wh, WTh, n, [t.shape for t in params])
+        ctx.keep = (spec, ix, net, ws, xc, tgt, p, Wh, WTh, n, [t.shape for t in params])
         return ws.out[:n].clone()
 
     @staticmethod
     def backward(ctx, grad_out):
         from .engine import SEG_ALIGN, round_up
         from ._lib import SirenGrads, ptr
-        spec, net, ws, xc, tgt, p, Wh, WTh, n, shapes = ctx.keep
+        spec, ix, net, ws, xc, tgt, p, Wh, WTh, n, shapes = ctx.keep
         lib = _lib.load()
         dev = xc.device
         L = spec.n_inner
@@ -183,10 +223,12 @@ class _SirenFunction(torch.autograd.Function):
         flat = torch.zeros(off + SEG_ALIGN, dtype=torch.float32, device=dev)
         views = [flat[o:o + int(np.prod(shp))].view(shp) for o, shp in zip(offs, shapes)]
         gs = SirenGrads()
-        gs.W0, gs.b0 = ptr(views[0]), ptr(views[1])
+        gs.W0, gs.b0 = ptr(views[ix["W0"]]), ptr(views[ix["b0"]])
         for i in range(L):
-            gs.W[i], gs.b[i] = ptr(views[2 + 2 * i]), ptr(views[3 + 2 * i])
-        gs.w_head, gs.b_head = ptr(views[2 + 2 * L]), ptr(views[3 + 2 * L])
+            gs.W[i], gs.b[i] = ptr(views[ix["W"][i]]), ptr(views[ix["b"][i]])
+            if ix["a"][i] is not None:
+                gs.a[i] = ptr(views[ix["a"][i]])
+        gs.w_head, gs.b_head = ptr(views[ix["wh"]]), ptr(views[ix["bh"]])
         gs.sse, gs.flat, gs.flat_len = flat.data_ptr() + 4 * off, ptr(flat), off + SEG_ALIGN
         b = ws.batch(xc, tgt, n, float(n))
         s = torch.cuda.current_stream(dev).cuda_stream

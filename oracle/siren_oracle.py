@@ -7,7 +7,8 @@ module, and only as the checker / the timed CPU baseline.  The product package
 A numpy restatement of the reference algorithm (senyuanfan/inr-for-audio):
   * get_coord / torch.linspace                utils.py:99-109
   * WaveformFitting target normalisation      utils.py:111-149
-  * SineLayer / SirenWithSnakeTanh forward    models.py:114-115, 388-394 (sine-only)
+  * SineLayer / SirenWithSnakeTanh forward    models.py:114-115, 388-394
+  * Linear + Snake / Linear + Tanh layers       models.py:235-241, 356-372
   * MSELoss + autograd backward               run.py:125,168,185
   * torch.optim.Adam step                     run.py:116,186
   * ReduceLROnPlateau(min, 0.8, 200)          run.py:117,187
@@ -92,38 +93,61 @@ def waveform_target(data: np.ndarray, duration: int, sample_rate: int, decimatio
 
 
 # ------------------------------------------------------------------ model (models.py)
-class Params:
-    """SIREN parameters in nn.Linear layout: W0 [H,in], b0 [H], W[i] [H,H], b[i] [H],
-    wf [H] (= net.{L+1}.weight[0]), bf scalar."""
+def layer_keys(num_sine: int, num_snake: int = 0, num_tanh: int = 0):
+    """state_dict keys of SirenWithSnakeTanh (models.py:306-386, first_linear=False,
+    last_linear=True): per inner layer (kind, weight, bias, a-or-None), then the head's
+    (weight, bias).  SineLayer i: net.{i}.linear.*; Linear+Snake: net.{j}.* + net.{j+1}.a;
+    Linear+Tanh: net.{j}.* (net.{j+1} is the parameterless Tanh)."""
+    layers, j = [], 1
+    for _ in range(num_sine):
+        layers.append(("sine", f"net.{j}.linear.weight", f"net.{j}.linear.bias", None))
+        j += 1
+    for kind in ["snake"] * num_snake + ["tanh"] * num_tanh:
+        layers.append((kind, f"net.{j}.weight", f"net.{j}.bias", f"net.{j + 1}.a" if kind == "snake" else None))
+        j += 2
+    return layers, (f"net.{j}.weight", f"net.{j}.bias")
 
-    def __init__(self, W0, b0, W, b, wf, bf):
+
+class Params:
+    """SirenWithSnakeTanh parameters in nn.Linear layout: W0 [H,in], b0 [H], W[i] [H,H],
+    b[i] [H], a[i] [H] (Snake layers, else None), wf [H] (= head weight[0]), bf scalar;
+    kinds[i] in {'sine', 'snake', 'tanh'}."""
+
+    def __init__(self, W0, b0, W, b, wf, bf, kinds=None, a=None):
         self.W0, self.b0 = np.asarray(W0, F32), np.asarray(b0, F32)
         self.W = [np.asarray(w, F32) for w in W]
         self.b = [np.asarray(x, F32) for x in b]
         self.wf = np.asarray(wf, F32).reshape(-1)
         self.bf = F32(np.asarray(bf).reshape(-1)[0])
+        self.kinds = list(kinds) if kinds is not None else ["sine"] * len(self.W)
+        self.a = [None if x is None else np.asarray(x, F32).reshape(-1) for x in (a or [None] * len(self.W))]
+
+    def counts(self):
+        return self.kinds.count("sine"), self.kinds.count("snake"), self.kinds.count("tanh")
 
     @classmethod
-    def from_state_dict(cls, sd: dict, n_inner: int):
+    def from_state_dict(cls, sd: dict, n_inner: int, num_snake: int = 0, num_tanh: int = 0):
+        """n_inner = num_sine (the sine-only form) when num_snake = num_tanh = 0."""
         g = lambda k: np.asarray(sd[k], F32)  # noqa: E731
-        return cls(g("net.0.linear.weight"), g("net.0.linear.bias"),
-                   [g(f"net.{i}.linear.weight") for i in range(1, n_inner + 1)],
-                   [g(f"net.{i}.linear.bias") for i in range(1, n_inner + 1)],
-                   g(f"net.{n_inner + 1}.weight"), g(f"net.{n_inner + 1}.bias"))
+        layers, (hw, hb) = layer_keys(n_inner, num_snake, num_tanh)
+        return cls(g("net.0.linear.weight"), g("net.0.linear.bias"), [g(w) for _, w, _, _ in layers],
+                   [g(b) for _, _, b, _ in layers], g(hw), g(hb), [k for k, _, _, _ in layers],
+                   [None if a is None else g(a) for _, _, _, a in layers])
 
     def to_state_dict(self) -> dict:
-        L = len(self.W)
+        layers, (hw, hb) = layer_keys(*self.counts())
         sd = {"net.0.linear.weight": self.W0, "net.0.linear.bias": self.b0}
-        for i in range(L):
-            sd[f"net.{i + 1}.linear.weight"] = self.W[i]
-            sd[f"net.{i + 1}.linear.bias"] = self.b[i]
-        sd[f"net.{L + 1}.weight"] = self.wf.reshape(1, -1)
-        sd[f"net.{L + 1}.bias"] = np.array([self.bf], F32)
+        for i, (_, wk, bk, ak) in enumerate(layers):
+            sd[wk] = self.W[i]
+            sd[bk] = self.b[i]
+            if ak is not None:
+                sd[ak] = self.a[i]
+        sd[hw] = self.wf.reshape(1, -1)
+        sd[hb] = np.array([self.bf], F32)
         return sd
 
     def flat(self) -> list[np.ndarray]:
-        return [self.W0, self.b0] + [x for pair in zip(self.W, self.b) for x in pair] + \
-               [self.wf.reshape(1, -1), np.array([self.bf], F32)]
+        return [np.asarray(v) for v in self.to_state_dict().values()]
 
 
 def first_preact(t: np.ndarray, W0: np.ndarray, b0: np.ndarray, omega0: float) -> np.ndarray:
@@ -154,19 +178,34 @@ def forward(p: Params, t: np.ndarray, omega0: float, omega: float, half: bool = 
     Y0 = sin32(A0)
     Y = [f16_round(Y0) if half else Y0]
     C0 = cos32(A0)
-    A, C = [A0], [f16_round(C0) if half else C0]
-    for Wi, bi in zip(p.W, p.b):
+    A, C, E = [A0], [f16_round(C0) if half else C0], [None]
+    for Wi, bi, kind, ai in zip(p.W, p.b, p.kinds, p.a):
         Wm = f16_round(Wi) if half else Wi
         z = np.asarray(Y[-1], dtype) @ np.asarray(Wm, dtype).T + np.asarray(bi, dtype)
-        a = (F64(omega) * np.asarray(z, F64)) if dtype == F64 else (F32(omega) * z.astype(F32))
-        y, c = np.sin(a), np.cos(a)
+        e = None
+        if kind == "sine":      # models.py:114-115
+            a = (F64(omega) * np.asarray(z, F64)) if dtype == F64 else (F32(omega) * z.astype(F32))
+            y, c = np.sin(a), np.cos(a)
+        elif kind == "snake":   # models.py:241 and its autograd: dY/dz, dY/da
+            a = np.asarray(z, F64)
+            av = np.asarray(ai, F64)[None, :]
+            s, cz = np.sin(av * a), np.cos(av * a)
+            y = a + s * s / av
+            c = 1.0 + 2.0 * s * cz
+            e = (a * 2.0 * s * cz) / av - s * s / (av * av)
+        else:                   # tanh, models.py:366-372
+            a = np.asarray(z, F64)
+            y = np.tanh(a)
+            c = 1.0 - y * y
         if half:
             y, c = f16_round(y), f16_round(c)
+            e = None if e is None else f16_round(e)
         A.append(a)
         Y.append(np.asarray(y, dtype if not half else F32))
         C.append(np.asarray(c, dtype if not half else F32))
+        E.append(None if e is None else np.asarray(e, dtype if not half else F32))
     out = np.asarray(Y[-1], dtype) @ np.asarray(p.wf, dtype) + dtype(p.bf)
-    return out, {"Y": Y, "A": A, "C": C}
+    return out, {"Y": Y, "A": A, "C": C, "E": E}
 
 
 def mse(out: np.ndarray, y: np.ndarray) -> float:
@@ -180,21 +219,30 @@ def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float
     nn.Linear layout (same keys as Params.to_state_dict).  With `half`, every dZ_i is
     rounded as the HIP path stores it: fp16(dZ_i * S) / S (exact power-of-two scale)."""
     L = len(p.W)
-    Y, A, C = cache["Y"], cache["A"], cache["C"]
-    S = grad_scale(g, p.wf, omega) if half else 1.0
+    Y, A, C, E = cache["Y"], cache["A"], cache["C"], cache.get("E", [None] * (L + 1))
+    layers, (hw, hb) = layer_keys(*p.counts())
+    # backward scale bound: |dY/dz| of the last layer (elementwise.hip grad_scale / capi act_bound)
+    bound = {"sine": omega, "snake": 2.0, "tanh": 1.0}[p.kinds[-1]]
+    S = grad_scale(g, p.wf, bound) if half else 1.0
     g = np.asarray(g, dtype).reshape(-1)
     grads = {}
-    grads[f"net.{L + 1}.weight"] = (g @ np.asarray(Y[L], dtype)).reshape(1, -1)
-    grads[f"net.{L + 1}.bias"] = np.array([g.sum()])
+    grads[hw] = (g @ np.asarray(Y[L], dtype)).reshape(1, -1)
+    grads[hb] = np.array([g.sum()])
     dY = g[:, None] * np.asarray(p.wf, dtype)[None, :]
     for i in range(L, 0, -1):
-        cos_i = np.asarray(C[i], dtype) if half else np.cos(np.asarray(A[i], F64)).astype(dtype)
-        dZ = dY * cos_i * dtype(omega)
+        kind, wk, bk, ak = layers[i - 1]
+        if kind == "sine":
+            cos_i = np.asarray(C[i], dtype) if half else np.cos(np.asarray(A[i], F64)).astype(dtype)
+            dZ = dY * cos_i * dtype(omega)
+        else:
+            dZ = dY * np.asarray(C[i], dtype)
+        if kind == "snake":
+            grads[ak] = (dY * np.asarray(E[i], dtype)).sum(0)
         db = dZ.sum(0)
         if half:
             dZ = (np.asarray(dZ * S, F32).astype(np.float16).astype(dtype) / S).astype(dtype)
-        grads[f"net.{i}.linear.weight"] = dZ.T @ np.asarray(Y[i - 1], dtype)
-        grads[f"net.{i}.linear.bias"] = db
+        grads[wk] = dZ.T @ np.asarray(Y[i - 1], dtype)
+        grads[bk] = db
         Wm = f16_round(p.W[i - 1]) if half else p.W[i - 1]
         dY = dZ @ np.asarray(Wm, dtype)
     cos0 = np.asarray(C[0], dtype) if half else np.cos(np.asarray(A[0], F64)).astype(dtype)
@@ -270,6 +318,7 @@ def reported_snr(ref_raw, fs, rec, duration, decimation=1) -> float:
 def fit(p: Params, t, y, omega0, omega, steps, lr=1e-3, min_lr=1e-6, half=False):
     """Full-batch fit with the restated loop; returns (params, losses, lrs)."""
     names = list(p.to_state_dict().keys())
+    counts = p.counts()
     flat = [x.astype(F32).copy() for x in p.to_state_dict().values()]
     ms = [np.zeros_like(x) for x in flat]
     vs = [np.zeros_like(x) for x in flat]
@@ -277,7 +326,7 @@ def fit(p: Params, t, y, omega0, omega, steps, lr=1e-3, min_lr=1e-6, half=False)
     losses, lrs = [], []
     L = len(p.W)
     for k in range(1, steps + 1):
-        cur = Params.from_state_dict(dict(zip(names, flat)), L)
+        cur = Params.from_state_dict(dict(zip(names, flat)), *counts)
         out, cache = forward(cur, t, omega0, omega, half=half)
         loss = F32(mse(out, y))
         grads = backward(cur, t, cache, mse_grad(out, y), omega0, omega, half=half)
@@ -286,4 +335,4 @@ def fit(p: Params, t, y, omega0, omega, steps, lr=1e-3, min_lr=1e-6, half=False)
                                               ms[j], vs[j], k, sched.lr)
         losses.append(float(loss))
         lrs.append(sched.step(loss))
-    return Params.from_state_dict(dict(zip(names, flat)), L), np.array(losses), np.array(lrs)
+    return Params.from_state_dict(dict(zip(names, flat)), *counts), np.array(losses), np.array(lrs)

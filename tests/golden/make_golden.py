@@ -93,6 +93,70 @@ def restated_loop(model, coords, target, steps, lr=1e-3, min_lr=1e-6):
     return np.array(losses), np.array(lrs), final
 
 
+def act_fixtures(ref_models, ref_utils, steps):
+    """Snake / Tanh layers (models.py:185-241, 356-372): init, one
+    forward/backward and a short full-batch trajectory of train()'s default architecture
+    (num_sine=2, num_snake=2, a_initial=0.5) plus a sine/Snake/Tanh mix and an a=None init."""
+    wav = os.path.join(REF, "gt_bach.wav")
+    coords, target = ref_utils.WaveformFitting(wav, duration=1, decimation=1)[0]
+    idx = np.arange(0, 44100, 21)
+    c_sub, t_sub = coords[idx], target[idx]
+    cfgs = {  # name: (H, num_sine, num_snake, num_tanh, omega0, a_initial, seed)
+        "default": (256, 2, 2, 0, 1000.0, 0.5, 1),
+        "mix": (128, 1, 2, 1, 1000.0, 0.5, 0),
+        "tanh": (128, 1, 0, 2, 1000.0, 0.5, 2),
+    }
+    fb = {"subset_idx": idx}
+    for name, (H, ns, nk, nt, w0, a0, seed) in cfgs.items():
+        torch.manual_seed(seed)
+        m = ref_models.SirenWithSnakeTanh(in_features=1, out_features=1, hidden_features=H, num_sine=ns,
+                                          num_snake=nk, num_tanh=nt, first_omega_0=w0, hidden_omega_0=30.0,
+                                          a_initial=a0)
+        for k, v in sd_np(m).items():
+            fb[f"{name}_init_{k}"] = v
+        out, loss, grads = fwd_bwd(m, c_sub, t_sub)
+        fb[f"{name}_out"] = out
+        fb[f"{name}_loss"] = np.array([loss])
+        for k, gr in grads.items():
+            fb[f"{name}_grad_{k}"] = gr
+    torch.manual_seed(4)
+    m = ref_models.SirenWithSnakeTanh(in_features=1, out_features=1, hidden_features=128, num_sine=1,
+                                      num_snake=1, num_tanh=0, first_omega_0=1000.0, a_initial=None)
+    for k, v in sd_np(m).items():
+        fb[f"expinit_init_{k}"] = v
+    np.savez_compressed(os.path.join(OUT, "fwd_bwd_act.npz"), **fb)
+    if steps > 0:
+        torch.manual_seed(1)
+        m = ref_models.SirenWithSnakeTanh(in_features=1, out_features=1, hidden_features=256, num_sine=2,
+                                          num_snake=2, num_tanh=0, first_omega_0=1000.0, a_initial=0.5)
+        losses, lrs, final = restated_loop(m, coords, target, steps)
+        tgt = target.numpy().reshape(-1)
+        json.dump({"steps": steps, "omega0": 1000.0, "hidden": 256, "num_sine": 2, "num_snake": 2,
+                   "a_initial": 0.5, "seed": 1, "loss": losses.tolist(), "lr": lrs.tolist(),
+                   "snr_target": float(ref_utils.calculate_snr(tgt, final))},
+                  open(os.path.join(OUT, "trajectory_snake_default.json"), "w"))
+        print(f"snake default: final loss {losses[-1]:.3e} min {losses.min():.3e}", flush=True)
+
+
+def snake_seed_trajectories(ref_models, ref_utils, seeds, steps):
+    """train()'s default architecture (num_sine=2, num_snake=2, a_initial=0.5, H=256,
+    omega0=1000) over several init seeds: loss / lr traces for the multi-seed fit protocol."""
+    wav = os.path.join(REF, "gt_bach.wav")
+    coords, target = ref_utils.WaveformFitting(wav, duration=1, decimation=1)[0]
+    tgt = target.numpy().reshape(-1)
+    out = {"steps": steps, "omega0": 1000.0, "hidden": 256, "num_sine": 2, "num_snake": 2,
+           "a_initial": 0.5, "runs": {}}
+    for s in seeds:
+        torch.manual_seed(s)
+        m = ref_models.SirenWithSnakeTanh(in_features=1, out_features=1, hidden_features=256, num_sine=2,
+                                          num_snake=2, num_tanh=0, first_omega_0=1000.0, a_initial=0.5)
+        losses, lrs, final = restated_loop(m, coords, target, steps)
+        out["runs"][str(s)] = {"loss": losses.tolist(), "lr": lrs.tolist(),
+                               "snr_target": float(ref_utils.calculate_snr(tgt, final))}
+        print(f"snake seed {s}: final {losses[-1]:.3e} min {losses.min():.3e}", flush=True)
+        json.dump(out, open(os.path.join(OUT, "trajectory_snake_default_seeds.json"), "w"))
+
+
 def seed_trajectories(ref_models, ref_utils, seeds, steps):
     """The full-batch trajectory of run.py:156-190 for several init seeds: at 300 steps the lr
     is still 1e-3 and late Adam loss spikes make one run's final SNR a random draw, so the
@@ -116,9 +180,18 @@ def main():
     ap.add_argument("--trajectory-steps", type=int, default=300)
     ap.add_argument("--seeds", default="0,1,2,3,4", help="init seeds of the multi-seed trajectories")
     ap.add_argument("--only-seeds", action="store_true", help="write only the multi-seed file")
+    ap.add_argument("--only-act", action="store_true", help="write only the Snake / Tanh fixtures")
+    ap.add_argument("--snake-seeds", default="", help="write only the Snake multi-seed trajectories")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 1)
     ref_models, ref_utils = import_reference()
+    if args.only_act:
+        act_fixtures(ref_models, ref_utils, args.trajectory_steps)
+        return
+    if args.snake_seeds:
+        snake_seed_trajectories(ref_models, ref_utils, [int(s) for s in args.snake_seeds.split(",")],
+                                args.trajectory_steps)
+        return
     if args.only_seeds:
         seed_trajectories(ref_models, ref_utils, [int(s) for s in args.seeds.split(",")],
                           args.trajectory_steps)
@@ -217,6 +290,7 @@ def main():
         np.savez_compressed(os.path.join(OUT, "trajectory_3x256_w1000_final.npz"), out=final.astype(np.float32))
         seed_trajectories(ref_models, ref_utils, [int(s) for s in args.seeds.split(",")],
                           args.trajectory_steps)
+    act_fixtures(ref_models, ref_utils, args.trajectory_steps)
     json.dump(meta, open(os.path.join(OUT, "meta.json"), "w"), indent=1)
     print("golden fixtures written to", OUT)
 

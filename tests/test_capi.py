@@ -35,7 +35,7 @@ def test_binding_table_matches_header(lib):
 
 
 def test_host_only_helpers(lib):
-    assert lib.siren_abi_version() == 2
+    assert lib.siren_abi_version() == 3
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256
@@ -68,4 +68,4 @@ def test_validation_without_device(lib):
 def test_supported_hidden_sizes_validate(lib, hidden):
     # only shape checks run (NULL outputs make it return before any launch)
     assert lib.siren_head_bwd(None, None, None, None, ctypes.c_float(30), 128, hidden, None, None, None,
-                              None, None) == 1002
+                              None, None, None, None) == 1002

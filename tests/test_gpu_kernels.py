@@ -220,7 +220,7 @@ def test_head_bwd(lib, dev, H, gmag, k):
     dwp = torch.empty(R // 128, H, device=dev)
     ok(lib.siren_head_bwd(ptr(to_dev(C, dev, H16)), ptr(to_dev(Y, dev, H16)),
                           ptr(to_dev(g, dev)), ptr(to_dev(w, dev)), ctypes.c_float(30.0), R, H,
-                          ptr(gscale_dev(dev, k)), ptr(dZ), ptr(dbp), ptr(dwp), S()), lib)
+                          ptr(gscale_dev(dev, k)), ptr(dZ), ptr(dbp), ptr(dwp), None, None, S()), lib)
     sc = 2.0 ** (k or 0)
     dz_ref = g[:, None].astype(np.float64) * w[None, :] * C * 30.0
     assert within_f16(f16_np(dZ), dz_ref * sc, 1e-12) <= 0

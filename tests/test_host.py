@@ -58,8 +58,8 @@ def test_hip_spec_validation():
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     spec = _model(256, 2, 22000.0).hip_spec()
     assert (spec.in_dim, spec.hidden, spec.n_inner, spec.omega0, spec.omega) == (1, 256, 2, 22000.0, 30.0)
-    bad = [dict(num_snake=2), dict(num_tanh=1), dict(first_linear=True), dict(last_linear=False),
-           dict(hidden_features=384), dict(num_sine=0), dict(in_features=3)]
+    bad = [dict(first_linear=True), dict(last_linear=False), dict(hidden_features=384),
+           dict(num_sine=0), dict(in_features=3), dict(num_sine=10, num_snake=4, num_tanh=3)]
     for kw in bad:
         args = dict(in_features=1, out_features=1, hidden_features=256, num_sine=2, num_snake=0, num_tanh=0)
         args.update(kw)
@@ -69,11 +69,22 @@ def test_hip_spec_validation():
 
 def test_reference_default_snake_config_constructs():
     """train()'s defaults (num_sine=2, num_snake=2, a_initial=0.5) build the reference's
-    module tree and parameter names even though the HIP path rejects Snake."""
+    module tree and parameter names, and the fused path's spec / parameter index."""
+    from inr_for_audio_amd import _lib
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     m = SirenWithSnakeTanh(1, 1, 256, 2, 2, 0, a_initial=0.5)
     names = list(m.state_dict().keys())
     assert names[-2:] == ["net.7.weight", "net.7.bias"] and "net.4.a" in names
+    spec = m.hip_spec()
+    assert spec.n_inner == 4 and spec.acts == (_lib.ACT_SINE,) * 2 + (_lib.ACT_SNAKE,) * 2
+    ix = m.param_index()
+    assert [names[k] for k in ix["W"]] == ["net.1.linear.weight", "net.2.linear.weight", "net.3.weight",
+                                          "net.5.weight"]
+    assert [None if k is None else names[k] for k in ix["a"]] == [None, None, "net.4.a", "net.6.a"]
+    assert (names[ix["wh"]], names[ix["bh"]]) == ("net.7.weight", "net.7.bias")
+    t = SirenWithSnakeTanh(2, 1, 128, 1, 1, 2, a_initial=None)
+    assert t.hip_spec().acts == (_lib.ACT_SINE, _lib.ACT_SNAKE, _lib.ACT_TANH, _lib.ACT_TANH)
+    assert [t.state_dict()[k].shape for k in ("net.3.a",)] == [(128,)]
 
 
 def test_shard_range_partitions():

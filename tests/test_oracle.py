@@ -150,3 +150,49 @@ def test_fit_tracks_reference_trajectory():
     ref = np.array(tr["loss"][:steps])
     assert np.max(np.abs(losses - ref) / ref) < 1e-3
     assert np.allclose(lrs, tr["lr"][:steps])
+
+
+# ---- Snake / Tanh layers: oracle pinned on the reference's own numbers ----
+ACT_CFGS = {"default": (2, 2, 0), "mix": (1, 2, 1), "tanh": (1, 0, 2)}
+
+
+def _act_params(name):
+    fb = load("fwd_bwd_act.npz")
+    pre = f"{name}_init_"
+    sd = {k[len(pre):]: fb[k] for k in fb.files if k.startswith(pre)}
+    return orc.Params.from_state_dict(sd, *ACT_CFGS[name]), sd
+
+
+def test_act_init_matches_reference():
+    """models.py mirror: same module tree, parameter names, init values (bit-exact) for
+    Snake(a) / Tanh stacks and the a=None Exponential init (models.py:224-229)."""
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    fb = load("fwd_bwd_act.npz")
+    cases = {"default": (256, 2, 2, 0, 0.5, 1), "mix": (128, 1, 2, 1, 0.5, 0), "tanh": (128, 1, 0, 2, 0.5, 2),
+             "expinit": (128, 1, 1, 0, None, 4)}
+    for name, (H, ns, nk, nt, a0, seed) in cases.items():
+        torch.manual_seed(seed)
+        m = SirenWithSnakeTanh(1, 1, H, ns, nk, nt, first_omega_0=1000.0, hidden_omega_0=30.0, a_initial=a0)
+        sd = m.state_dict()
+        pre = f"{name}_init_"
+        ref = {k[len(pre):]: fb[k] for k in fb.files if k.startswith(pre)}
+        assert list(sd.keys()) == list(ref.keys()), name
+        for k, v in sd.items():
+            assert np.array_equal(v.numpy(), ref[k]), (name, k)
+
+
+@pytest.mark.parametrize("name", list(ACT_CFGS))
+def test_act_forward_backward_matches_reference(name):
+    fb = load("fwd_bwd_act.npz")
+    t, y = _subset()
+    p, sd = _act_params(name)
+    out, cache = orc.forward(p, t, 1000.0, 30.0, dtype=np.float64)
+    ref = fb[f"{name}_out"]
+    assert np.max(np.abs(out - ref)) < 1e-5 * max(1.0, np.max(np.abs(ref)))
+    assert abs(orc.mse(out, y) - float(fb[f"{name}_loss"][0])) < 1e-5 * float(fb[f"{name}_loss"][0])
+    grads = orc.backward(p, t, cache, orc.mse_grad(out, y), 1000.0, 30.0)
+    assert set(grads) == set(sd)
+    for k, g in grads.items():
+        r = fb[f"{name}_grad_{k}"]
+        rel = np.linalg.norm(np.asarray(g).reshape(r.shape) - r) / np.linalg.norm(r)
+        assert rel < 1e-4, (name, k, rel)
