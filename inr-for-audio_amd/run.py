@@ -3,9 +3,14 @@
 Differences from the reference are limited to what the hot-path scope excludes: no plots
 (matplotlib figures), no loss-landscape, no STFT/MAE/SNR loss mixes (alpha must be 0 and
 loss_mode 'mse' -- at alpha=0 the reference's STFT term contributes exactly zero, SURVEY
-§8 a8), no random-Fourier-feature encoding, no KAN, no MDCT target yet.
-Everything the path produces -- output.wav, the checkpoint dict, parameters.json with the
-run.py-formula SNR -- keeps the reference's names and formats.
+§8 a8), no random-Fourier-feature encoding, no KAN.  method='mdct' fits the
+MDCT-domain target (utils.MDCTFitting, N = 2048, mode='log' = takelog) with
+(bin, frame) coordinates and inverts it as run.py:258-290 does.  Everything the path
+produces -- output.wav, the checkpoint dict, parameters.json with the run.py-formula SNR --
+keeps the reference's names and formats.  One deliberate deviation: for method='mdct' the
+reference's final SNR line (run.py:335) raises a numpy broadcast error whenever
+fs * duration is not a multiple of N/2 (the recovered signal has frames * N/2 samples);
+here the SNR is taken over the common length instead.
 """
 from __future__ import annotations
 
@@ -19,7 +24,8 @@ import torch
 
 from .engine import SirenEngine
 from .models import SirenWithSnakeTanh
-from .utils import WaveformFitting, calculate_snr, get_coord, load_mono_like_librosa, reported_snr
+from .utils import (MDCTFitting, WaveformFitting, calculate_snr, get_coord, load_mono_like_librosa,
+                    reported_snr)
 
 
 def save_parameters(experiment_folder, **kwargs):
@@ -44,8 +50,10 @@ def train(experiment_path: str, tag: str, inst: str, duration: int, num_channels
     ``filename`` (default ``{data_dir}/{inst}.wav`` as run.py:33), ``seed`` (torch.manual_seed
     before model construction), ``micro_batch`` (rows per fused micro-batch), ``use_graph``
     (replay each step as a HIP graph), ``device``."""
-    if method != "wave":
-        raise NotImplementedError("method='mdct' is SURVEY §8 f2 (not on the HIP path yet)")
+    if method not in ("wave", "mdct"):
+        raise ValueError("specify the correct fitting method as wave or mdct (run.py:77-78)")
+    if method == "mdct" and bwe:
+        raise NotImplementedError("bwe is a waveform-mode feature (run.py:127-131)")
     if arch != "mlp":
         raise NotImplementedError("arch='kan' is SURVEY §8 f4 (not on the HIP path yet)")
     if loss_mode != "mse" or alpha != 0.0:
@@ -65,9 +73,18 @@ def train(experiment_path: str, tag: str, inst: str, duration: int, num_channels
         os.makedirs(experiment_folder)
     decimation = int(decimation)
 
-    input_data = WaveformFitting(filename, duration=duration, decimation=decimation)
-    model_input, ground_truth = input_data[0]
-    input_dimension = 1
+    takelog = False
+    if method == "wave":
+        input_data = WaveformFitting(filename, duration=duration, decimation=decimation)
+        model_input, ground_truth = input_data[0]
+        input_dimension = 1
+    else:  # run.py:67-76
+        N = 2048
+        takelog = mode == "log"
+        input_data = MDCTFitting(filename, duration=duration, N=N, takelog=takelog)
+        model_input, pixels = input_data[0]
+        ground_truth = torch.from_numpy(np.ascontiguousarray(pixels))
+        input_dimension = 2
 
     if seed is not None:
         torch.manual_seed(seed)
@@ -118,7 +135,11 @@ def train(experiment_path: str, tag: str, inst: str, duration: int, num_channels
     else:
         coords = model_input
         recover_sample_rate = input_data.sample_rate
-    signal_recovered = engine.infer(coords.to(dev)).cpu().numpy().astype(np.float32)
+    model_output = engine.infer(coords.to(dev)).cpu().numpy().astype(np.float32)
+    if method == "wave":
+        signal_recovered = model_output
+    else:  # run.py:258-259, 281-290 (double exp in log mode)
+        signal_recovered = input_data.to_signal(model_output, takelog=takelog).reshape(-1)
 
     ckpt_path = f"{experiment_folder}/saved_ckpt.pt"
     if rank0:
@@ -126,9 +147,13 @@ def train(experiment_path: str, tag: str, inst: str, duration: int, num_channels
         wavfile.write(output_filename, recover_sample_rate, signal_recovered.reshape(-1, 1))
         ref, fs_ref = load_mono_like_librosa(filename)
         rec, _ = load_mono_like_librosa(output_filename)
+        if method == "mdct":
+            m = min(int(fs_ref * duration), len(rec))
+            ref, rec = ref[:m], rec[:m]
         snr_final = float(reported_snr(ref, fs_ref, rec, duration, decimation, bwe))
         target = ground_truth.numpy().reshape(-1)
-        snr_target = float(calculate_snr(target, signal_recovered)) if not bwe else None
+        # the fit in its own (training) domain: waveform or normalised MDCT map
+        snr_target = float(calculate_snr(target, model_output)) if not bwe else None
 
         checkpoint = {"model_state_dict": {k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
                       "optimizer_state_dict": engine.adam_state_dict()}

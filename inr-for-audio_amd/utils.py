@@ -94,3 +94,71 @@ def reported_snr(ref_raw, fs_ref, rec, duration, decimation=1, bwe=False):
     ref = decimate(ref, q=d)
     ref = ref + 1e-10
     return calculate_snr(ref, rec)
+
+
+def hpfilter(data, cutoff, fs):
+    """5th-order Butterworth high-pass, zero-phase (utils.py:49-52)."""
+    from scipy.signal import butter, filtfilt
+    b, a = butter(5, cutoff, btype="highpass", fs=fs)
+    return filtfilt(b, a, data)
+
+
+class MDCTFitting:
+    """MDCT-domain fitting target -- utils.py:312-414.
+
+    The clip (channel 1 of a multi-channel file, as the reference reads it) is divided by
+    max|x| over the WHOLE file, trimmed to `duration` seconds, and transformed by STMDCT
+    (N-sample KBD frames hopping N/2) into a [N/2 bins][frames] float32 map; optionally
+    shifted positive and log-compressed (takelog); then mean-removed and scaled by its max
+    |.|.  Coordinates are the (bin, frame) linspace grid, bin-major: (height*width, 2)."""
+
+    def __init__(self, filename=None, duration=1, N=1024, highpass=False, takelog=False, *,
+                 data=None, sample_rate=None):
+        from . import mdct
+        if data is None:
+            self.sample_rate, self.data = wavfile.read(filename)
+        else:
+            self.sample_rate, self.data = int(sample_rate), np.asarray(data)
+        self.original_sample_rate = self.sample_rate
+        if len(self.data.shape) > 1:
+            self.data = self.data[:, 1]
+        if highpass:
+            self.data = hpfilter(self.data, 150, self.sample_rate)
+        self.data = torch.from_numpy(self.data.astype(np.float32)[:duration * self.sample_rate]
+                                     / np.max(np.abs(self.data)))
+        self.N = N
+        self.mdct = mdct.STMDCT(self.data.numpy(), N=N).astype(np.float32)
+        self.shift = 0.0
+        if takelog:
+            self.shift = np.abs(np.min(self.mdct)) + 1e-8
+            self.mdct = np.log(self.mdct + self.shift)
+        self.mean = np.mean(self.mdct)
+        self.mdct = self.mdct - self.mean
+        self.scale = np.max(np.abs(self.mdct))
+        self.mdct = self.mdct / self.scale
+        self.height, self.width = self.mdct.shape
+        h_grid, w_grid = torch.meshgrid(torch.linspace(-1, 1, steps=self.height),
+                                        torch.linspace(-1, 1, steps=self.width), indexing="ij")
+        self.coords = torch.stack((h_grid, w_grid), dim=-1).reshape(self.height * self.width, -1)
+        self.pixels = self.mdct.reshape(-1, 1)
+
+    def __len__(self):
+        return 1
+
+    def __getitem__(self, idx):
+        if idx > 0:
+            raise IndexError
+        return self.coords, self.pixels
+
+    def to_signal(self, model_output, takelog=False):
+        """run.py:258-259 + 281-290: normalised model output [height*width] -> waveform.
+        With takelog the reference exponentiates TWICE -- once on the raw output, once after
+        de-normalisation -- and so does this (drop-in fidelity)."""
+        from . import mdct
+        out = np.asarray(model_output, dtype=np.float32).reshape(-1)
+        if takelog:
+            out = np.exp(out)
+        spec = out.reshape(self.height, self.width) * self.scale + self.mean - self.shift
+        if takelog:
+            spec = np.exp(spec)
+        return mdct.ISTMDCT(spec, N=self.N).reshape(-1, 1).astype(np.float32)

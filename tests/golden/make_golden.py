@@ -76,7 +76,7 @@ def restated_loop(model, coords, target, steps, lr=1e-3, min_lr=1e-6):
     sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.8, patience=200,
                                                        min_lr=min_lr)
     mse = torch.nn.MSELoss()
-    x = coords.reshape(1, -1, 1)
+    x = coords.reshape(1, coords.shape[0], -1)
     y = target.reshape(1, -1, 1)
     losses, lrs = [], []
     for _ in range(steps):
@@ -138,6 +138,56 @@ def act_fixtures(ref_models, ref_utils, steps):
         print(f"snake default: final loss {losses[-1]:.3e} min {losses.min():.3e}", flush=True)
 
 
+def mdct_fixtures(ref_models, steps):
+    """MDCT-domain target: the reference's STMDCT / ISTMDCT on a seeded signal
+    (mdct.py), MDCTFitting on gt_bach 1 s with N = 2048 (utils.py:312-414, takelog off / on),
+    the run.py:258-290 inversion of a synthetic model output, and a short full-batch fit of
+    a SIREN 5x512 on the (bin, frame) grid (in = 2)."""
+    import contextlib
+    import io
+    import mdct as ref_mdct  # noqa: E402  (the reference's own module)
+    import utils as ref_utils  # noqa: E402
+    rng = np.random.default_rng(7)
+    x = rng.uniform(-1, 1, 5000).astype(np.float32)
+    kat = {"x": x}
+    for N in (1024, 2048):
+        c = ref_mdct.STMDCT(x, N=N)
+        kat[f"stmdct_{N}"] = c
+        kat[f"istmdct_{N}"] = ref_mdct.ISTMDCT(c, N=N)
+    np.savez_compressed(os.path.join(OUT, "mdct_kat.npz"), **kat)
+    wav = os.path.join(REF, "gt_bach.wav")
+    fit = {}
+    for takelog in (False, True):
+        with contextlib.redirect_stdout(io.StringIO()):
+            d = ref_utils.MDCTFitting(wav, duration=1, N=2048, takelog=takelog)
+        tag = "log" if takelog else "lin"
+        fit[f"{tag}_pixels"] = d.pixels.reshape(-1)
+        fit[f"{tag}_stats"] = np.array([d.mean, d.scale, d.shift, d.height, d.width], np.float64)
+        # run.py:258-259 and 281-290 applied to a synthetic model output
+        out = (0.9 * d.pixels.reshape(-1) + 0.01 * np.sin(np.arange(d.pixels.size))).astype(np.float32)
+        o = torch.from_numpy(out)
+        if takelog:
+            o = torch.exp(o)
+        spec = (o.reshape(d.height, d.width) * d.scale + d.mean - d.shift).numpy()
+        if takelog:
+            spec = np.exp(spec)
+        fit[f"{tag}_model_out"] = out
+        fit[f"{tag}_signal"] = ref_mdct.ISTMDCT(spec, N=2048).reshape(-1).astype(np.float32)
+        if not takelog:
+            coords = d.coords
+            target = torch.from_numpy(d.pixels)
+    np.savez_compressed(os.path.join(OUT, "mdct_fitting_1s.npz"), **fit)
+    if steps > 0:
+        torch.manual_seed(0)
+        m = ref_models.SirenWithSnakeTanh(in_features=2, out_features=1, hidden_features=512, num_sine=4,
+                                          num_snake=0, num_tanh=0, first_omega_0=1000.0, hidden_omega_0=30.0)
+        losses, lrs, _ = restated_loop(m, coords, target, steps)
+        json.dump({"steps": steps, "omega0": 1000.0, "hidden": 512, "num_sine": 4, "seed": 0, "N": 2048,
+                   "loss": losses.tolist(), "lr": lrs.tolist()},
+                  open(os.path.join(OUT, "trajectory_mdct_5x512.json"), "w"))
+        print(f"mdct 5x512: losses {losses[:3]} ... {losses[-1]:.3e}", flush=True)
+
+
 def snake_seed_trajectories(ref_models, ref_utils, seeds, steps):
     """train()'s default architecture (num_sine=2, num_snake=2, a_initial=0.5, H=256,
     omega0=1000) over several init seeds: loss / lr traces for the multi-seed fit protocol."""
@@ -182,11 +232,15 @@ def main():
     ap.add_argument("--only-seeds", action="store_true", help="write only the multi-seed file")
     ap.add_argument("--only-act", action="store_true", help="write only the Snake / Tanh fixtures")
     ap.add_argument("--snake-seeds", default="", help="write only the Snake multi-seed trajectories")
+    ap.add_argument("--only-mdct", action="store_true", help="write only the MDCT fixtures")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 1)
     ref_models, ref_utils = import_reference()
     if args.only_act:
         act_fixtures(ref_models, ref_utils, args.trajectory_steps)
+        return
+    if args.only_mdct:
+        mdct_fixtures(ref_models, args.trajectory_steps)
         return
     if args.snake_seeds:
         snake_seed_trajectories(ref_models, ref_utils, [int(s) for s in args.snake_seeds.split(",")],
@@ -291,6 +345,7 @@ def main():
         seed_trajectories(ref_models, ref_utils, [int(s) for s in args.seeds.split(",")],
                           args.trajectory_steps)
     act_fixtures(ref_models, ref_utils, args.trajectory_steps)
+    mdct_fixtures(ref_models, 20)
     json.dump(meta, open(os.path.join(OUT, "meta.json"), "w"), indent=1)
     print("golden fixtures written to", OUT)
 

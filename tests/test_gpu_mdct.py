@@ -1,0 +1,82 @@
+"""MDCT-domain fit (utils.py:312-414, run.py:67-76, 258-290) on the HIP path:
+the same fused SIREN kernels with (bin, frame) coordinates (in = 2).  The first steps track
+the reference's own full-batch loop on the same target (tests/golden/trajectory_mdct_5x512.json),
+and train(method='mdct') runs end to end with the reference's artifacts."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+from scipy.io import wavfile
+
+from oracle import siren_oracle as orc
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _clip():
+    g = np.load(os.path.join(G, "gt_bach_1s.npz"))
+    return np.concatenate([g["raw"], np.array([1.0], np.float32)]), int(g["fs"])
+
+
+def _model(seed=0):
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(seed)
+    return SirenWithSnakeTanh(2, 1, 512, 4, 0, 0, first_omega_0=1000.0, hidden_omega_0=30.0)
+
+
+def test_mdct_step_grads_vs_oracle(dev):
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.utils import MDCTFitting
+    data, fs = _clip()
+    d = MDCTFitting(duration=1, N=2048, data=data, sample_rate=fs)
+    m = _model()
+    sd0 = {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}
+    # a 4096-coordinate slice of the (bin, frame) grid keeps the fp64 oracle quick
+    t, y = d.coords[:4096], torch.from_numpy(d.pixels[:4096])
+    eng = SirenEngine(m, t, y, device=dev)
+    eng.step()
+    torch.cuda.synchronize()
+    got = {k: v.detach().cpu().numpy() for k, v in zip(eng.layout.names, eng.grad_views())}
+    p = orc.Params.from_state_dict(sd0, 4)
+    out, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
+    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), 1000.0, 30.0, half=True)
+    for k, r in ref.items():
+        rel = np.linalg.norm(got[k].reshape(r.shape) - r) / np.linalg.norm(r)
+        assert rel < 2e-2, (k, rel)
+
+
+def test_mdct_fit_first_steps_track_reference(dev):
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.utils import MDCTFitting
+    tr = json.load(open(os.path.join(G, "trajectory_mdct_5x512.json")))
+    data, fs = _clip()
+    d = MDCTFitting(duration=1, N=2048, data=data, sample_rate=fs)
+    eng = SirenEngine(_model(tr["seed"]), d.coords, torch.from_numpy(d.pixels), lr=1e-3, device=dev)
+    for _ in range(tr["steps"]):
+        eng.step()
+    losses, lrs = eng.history()
+    ref = np.array(tr["loss"])
+    assert np.max(np.abs(losses[:3] - ref[:3]) / ref[:3]) < 5e-2, (losses[:5], ref[:5])
+    assert np.array_equal(lrs, np.array(tr["lr"]))
+
+
+@pytest.mark.parametrize("mode", [None, "log"])
+def test_train_mdct_end_to_end(dev, tmp_path, mode):
+    from inr_for_audio_amd.run import train
+    data, fs = _clip()
+    wav = tmp_path / "clip.wav"
+    wavfile.write(wav, fs, data)
+    ckpt = train(str(tmp_path), "t", "clip", 1, method="mdct", mode=mode, num_hidden_features=256,
+                 num_sine=2, num_snake=1, omega=1000, total_steps=40, filename=str(wav), seed=0)
+    folder = os.path.dirname(ckpt)
+    sr, out = wavfile.read(os.path.join(folder, "output.wav"))
+    assert sr == fs and out.dtype == np.float32 and out.shape[0] == 43 * 1024
+    assert np.all(np.isfinite(out))
+    params = json.load(open(os.path.join(folder, "parameters.json")))
+    assert params["method"] == "mdct" and params["mode"] == mode and np.isfinite(params["SNR"])
+    assert np.isfinite(params["SNR_target"])
+    sd = torch.load(ckpt, weights_only=True)
+    assert "net.4.a" in sd["model_state_dict"] and sd["model_state_dict"]["net.0.linear.weight"].shape == (256, 2)
