@@ -209,6 +209,47 @@ int siren_plateau_step(siren_opt_state* state, const float* sse, double n_total,
 int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wh, uint16_t* WTh,
                       void* stream);
 
+/* ---- KAN variant: run.py:92-93 KAN([in, H, H, 1]) of kan.py:169-285 ----------
+ * Layer l maps width[l] -> width[l+1] as efficient-KAN's KANLinear (kan.py:6-166) with
+ * grid_size 5, spline_order 3, SiLU base: out = SiLU(x) base_w^T + B(x) (spline_w*scaler)^T,
+ * B = the 8 order-3 B-spline bases on the layer's `grid` buffer [in][12].  fp32 throughout.
+ * The last width must be 1.  Workspace: one caller-owned fp32 buffer of
+ * siren_kan_workspace_floats(net, rows, splits) floats (activations, expansions, combined
+ * weights, split-K slabs). */
+#define SIREN_KAN_MAX_LAYERS 8
+typedef struct siren_kan_net {
+  int32_t n_layers, pad0;
+  int32_t width[SIREN_KAN_MAX_LAYERS + 1];
+  const float* grid[SIREN_KAN_MAX_LAYERS];      /* [in][12]     buffer layers.l.grid        */
+  const float* base_w[SIREN_KAN_MAX_LAYERS];    /* [out][in]    layers.l.base_weight        */
+  const float* spline_w[SIREN_KAN_MAX_LAYERS];  /* [out][in][8] layers.l.spline_weight      */
+  const float* scaler[SIREN_KAN_MAX_LAYERS];    /* [out][in]    layers.l.spline_scaler      */
+} siren_kan_net;
+typedef struct siren_kan_grads {
+  float* base_w[SIREN_KAN_MAX_LAYERS];
+  float* spline_w[SIREN_KAN_MAX_LAYERS];
+  float* scaler[SIREN_KAN_MAX_LAYERS];
+  float* sse;                               /* [1] sum of squared errors of valid rows */
+  float* flat; int64_t flat_len;            /* if flat != NULL and zero_grads: memset   */
+} siren_kan_grads;
+typedef struct siren_kan_batch {
+  int32_t rows, n_valid;    /* rows: any count >= n_valid (no padding needed)      */
+  double n_total;           /* global coordinate count (MSE mean denominator)      */
+  int32_t splits;           /* split-K slices of the weight-gradient GEMMs (>= 1)  */
+  int32_t zero_grads;
+  const float* coords;      /* [rows][width[0]]  */
+  const float* target;      /* [rows]            */
+  float* out;               /* [rows] model output                                */
+  float* g;                 /* [rows] dLoss/dout                                  */
+  float* ws;                /* workspace, siren_kan_workspace_floats() floats     */
+} siren_kan_batch;
+int64_t siren_kan_workspace_floats(const siren_kan_net* net, int32_t rows, int32_t splits);
+/* run.py:255 model(model_input) for arch='kan' */
+int siren_kan_forward(const siren_kan_net* net, siren_kan_batch* batch, void* stream);
+/* run.py:158-185 for arch='kan': forward + MSELoss + backward; gradients ACCUMULATE */
+int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* grads, siren_kan_batch* batch,
+                         void* stream);
+
 /* ---- per-launch HIP-event profiling of the fused path (bench.py) --------------------
  * siren_profile_enable(n) creates 2n hipEvents; while enabled every launch made by
  * siren_train_step / siren_backward / siren_forward / siren_apply_update is bracketed

@@ -69,6 +69,31 @@ class SirenBatch(ctypes.Structure):
     ]
 
 
+KAN_MAX_LAYERS = 8
+
+
+class SirenKanNet(ctypes.Structure):
+    _fields_ = [
+        ("n_layers", _i32), ("pad0", _i32), ("width", _i32 * (KAN_MAX_LAYERS + 1)),
+        ("grid", _p * KAN_MAX_LAYERS), ("base_w", _p * KAN_MAX_LAYERS),
+        ("spline_w", _p * KAN_MAX_LAYERS), ("scaler", _p * KAN_MAX_LAYERS),
+    ]
+
+
+class SirenKanGrads(ctypes.Structure):
+    _fields_ = [
+        ("base_w", _p * KAN_MAX_LAYERS), ("spline_w", _p * KAN_MAX_LAYERS), ("scaler", _p * KAN_MAX_LAYERS),
+        ("sse", _p), ("flat", _p), ("flat_len", _i64),
+    ]
+
+
+class SirenKanBatch(ctypes.Structure):
+    _fields_ = [
+        ("rows", _i32), ("n_valid", _i32), ("n_total", ctypes.c_double), ("splits", _i32),
+        ("zero_grads", _i32), ("coords", _p), ("target", _p), ("out", _p), ("g", _p), ("ws", _p),
+    ]
+
+
 # name -> (restype, argtypes).  Mirrors include/siren_hip.h one-to-one; the CPU test
 # suite checks that every symbol the header declares is exported.
 _SIGS = {
@@ -108,6 +133,10 @@ _SIGS = {
     "siren_plateau_step": (ctypes.c_int, [_p, _p, ctypes.c_double, _p, _p, _i64, _p]),
     "siren_cast_weight": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p]),
     "siren_set_option": (ctypes.c_int, [_i32, _i32]),
+    "siren_kan_workspace_floats": (_i64, [ctypes.POINTER(SirenKanNet), _i32, _i32]),
+    "siren_kan_forward": (ctypes.c_int, [ctypes.POINTER(SirenKanNet), ctypes.POINTER(SirenKanBatch), _p]),
+    "siren_kan_train_step": (ctypes.c_int, [ctypes.POINTER(SirenKanNet), ctypes.POINTER(SirenKanGrads),
+                                            ctypes.POINTER(SirenKanBatch), _p]),
     "siren_profile_enable": (ctypes.c_int, [_i32]),
     "siren_profile_reset": (ctypes.c_int, []),
     "siren_profile_read": (ctypes.c_int, [_i32, ctypes.POINTER(ctypes.c_double),

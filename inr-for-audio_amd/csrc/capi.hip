@@ -534,3 +534,145 @@ int siren_profile_read(int32_t kind, double* total_ms, int64_t* count) {
 }
 
 }  // extern "C"
+
+// ---- KAN variant (kan.py, run.py:92-93) -----------------------------------
+namespace {
+
+constexpr int KAN_K1 = 9;  // A-columns per input feature: SiLU + 8 B-spline bases
+
+int check_kan(const siren_kan_net* n) {
+  if (!n) return SIREN_ERR_NULL;
+  if (n->n_layers < 1 || n->n_layers > SIREN_KAN_MAX_LAYERS) return SIREN_ERR_CONFIG;
+  for (int l = 0; l <= n->n_layers; ++l)
+    if (n->width[l] < 1 || n->width[l] > 4096) return SIREN_ERR_SHAPE;
+  if (n->width[n->n_layers] != 1) return SIREN_ERR_SHAPE;
+  for (int l = 0; l < n->n_layers; ++l)
+    if (!n->grid[l] || !n->base_w[l] || !n->spline_w[l] || !n->scaler[l]) return SIREN_ERR_NULL;
+  return SIREN_OK;
+}
+
+// Workspace carve-up (floats, each piece 64-float aligned):
+//   A[l] rows x 9 w[l];  X[l] rows x w[l] for l = 1..L (X[L] = the output row vector);
+//   W[l] w[l+1] x 9 w[l];  dW w_max_out x 9 w_max_in;  slab splits x that;  dA rows x 9 w_max;
+//   G[2] rows x w_max;  sse/gsum/gmax partials 3 x ceil(rows/256);  one zero float.
+struct KanWs {
+  float* A[SIREN_KAN_MAX_LAYERS];
+  float* X[SIREN_KAN_MAX_LAYERS + 1];
+  float* W[SIREN_KAN_MAX_LAYERS];
+  float *dW, *slab, *dA, *G[2], *sse_part, *gsum_part, *gmax_part, *zero;
+  int64_t total;
+};
+
+inline int64_t al64(int64_t x) { return (x + 63) / 64 * 64; }
+
+KanWs kan_layout(const siren_kan_net* n, int64_t rows, int splits, float* base) {
+  KanWs w = {};
+  int64_t off = 0;
+  auto take = [&](int64_t floats) {
+    float* p = base ? base + off : nullptr;
+    off += al64(floats);
+    return p;
+  };
+  int64_t wmax = 1, wk = 1;
+  for (int l = 0; l < n->n_layers; ++l) {
+    w.A[l] = take(rows * KAN_K1 * n->width[l]);
+    w.W[l] = take((int64_t)n->width[l + 1] * KAN_K1 * n->width[l]);
+    const int64_t kw = (int64_t)n->width[l + 1] * KAN_K1 * n->width[l];
+    if (kw > wk) wk = kw;
+    if (n->width[l] > wmax) wmax = n->width[l];
+  }
+  for (int l = 1; l <= n->n_layers; ++l) w.X[l] = take(rows * n->width[l]);
+  w.dW = take(wk);
+  w.slab = take(wk * splits);
+  w.dA = take(rows * KAN_K1 * wmax);
+  w.G[0] = take(rows * wmax);
+  w.G[1] = take(rows * wmax);
+  const int64_t np = (rows + 255) / 256;
+  w.sse_part = take(np);
+  w.gsum_part = take(np);
+  w.gmax_part = take(np);
+  w.zero = take(1);
+  w.total = off;
+  return w;
+}
+
+hipError_t kan_run_forward(const siren_kan_net* n, const siren_kan_batch* b, const KanWs& w, hipStream_t s) {
+  const int64_t R = b->rows;
+  const float* x = b->coords;
+  for (int l = 0; l < n->n_layers; ++l) {
+    const int in = n->width[l], out = n->width[l + 1];
+    const int64_t K = (int64_t)KAN_K1 * in;
+    hipError_t e = kan_expand(x, n->grid[l], R, in, w.A[l], s);
+    if (e == hipSuccess) e = kan_combine(n->base_w[l], n->spline_w[l], n->scaler[l], out, in, w.W[l], s);
+    // X[l+1][r][o] = sum_k A[r][k] W[o][k]
+    if (e == hipSuccess) e = kan_gemm(w.A[l], K, 1, w.W[l], 1, K, (int)R, out, K, 1, nullptr, w.X[l + 1], s);
+    if (e != hipSuccess) return e;
+    x = w.X[l + 1];
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t siren_kan_workspace_floats(const siren_kan_net* net, int32_t rows, int32_t splits) {
+  if (check_kan(net) || rows < 1 || splits < 1) return -1;
+  return kan_layout(net, rows, splits, nullptr).total;
+}
+
+int siren_kan_forward(const siren_kan_net* net, siren_kan_batch* b, void* stream) {
+  int st = check_kan(net);
+  if (st) return st;
+  if (!b) return SIREN_ERR_NULL;
+  if (!b->coords || !b->out || !b->g || !b->ws) return SIREN_ERR_NULL;
+  if (b->rows < 1 || b->splits < 1) return SIREN_ERR_SHAPE;
+  hipStream_t s = S(stream);
+  const KanWs w = kan_layout(net, b->rows, b->splits, b->ws);
+  SIREN_TRY(hipMemsetAsync(w.zero, 0, sizeof(float), s));
+  SIREN_TRY(kan_run_forward(net, b, w, s));
+  SIREN_TRY(head_loss(w.X[net->n_layers], 1, b->rows, w.zero, b->out, 0, 0.f, b->out, b->g, w.sse_part,
+                      w.gsum_part, nullptr, s));
+  return SIREN_OK;
+}
+
+int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, siren_kan_batch* b, void* stream) {
+  int st = check_kan(net);
+  if (st) return st;
+  if (!b || !gr || !gr->sse) return SIREN_ERR_NULL;
+  if (!b->coords || !b->target || !b->out || !b->g || !b->ws) return SIREN_ERR_NULL;
+  if (b->rows < 1 || b->splits < 1 || b->n_valid < 0 || b->n_valid > b->rows || b->n_total <= 0)
+    return SIREN_ERR_SHAPE;
+  for (int l = 0; l < net->n_layers; ++l)
+    if (!gr->base_w[l] || !gr->spline_w[l] || !gr->scaler[l]) return SIREN_ERR_NULL;
+  hipStream_t s = S(stream);
+  const int64_t R = b->rows;
+  const KanWs w = kan_layout(net, R, b->splits, b->ws);
+  if (b->zero_grads && gr->flat) SIREN_TRY(hipMemsetAsync(gr->flat, 0, gr->flat_len * sizeof(float), s));
+  SIREN_TRY(hipMemsetAsync(w.zero, 0, sizeof(float), s));
+  SIREN_TRY(kan_run_forward(net, b, w, s));
+  // MSELoss (run.py:168): out, g = 2(out - y)/N_total, squared-error partials
+  SIREN_TRY(head_loss(w.X[net->n_layers], 1, b->rows, w.zero, b->target, b->n_valid,
+                      (float)(2.0 / b->n_total), b->out, b->g, w.sse_part, w.gsum_part, w.gmax_part, s));
+  SIREN_TRY(sum_to(w.sse_part, (int)((R + 255) / 256), gr->sse, 1, s));
+  // backward (autograd of run.py:185): G = dLoss/dX[l+1], [R][out]
+  const float* G = b->g;
+  int cur = 0;
+  for (int l = net->n_layers - 1; l >= 0; --l) {
+    const int in = net->width[l], out = net->width[l + 1];
+    const int64_t K = (int64_t)KAN_K1 * in;
+    // dW[o][k] = sum_r G[r][o] A[r][k]  (split-K over the coordinates)
+    SIREN_TRY(kan_gemm(G, 1, out, w.A[l], K, 1, out, (int)K, R, b->splits, w.slab, w.dW, s));
+    SIREN_TRY(kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1, gr->base_w[l], gr->spline_w[l],
+                              gr->scaler[l], s));
+    if (l == 0) break;
+    // dA[r][k] = sum_o G[r][o] W[o][k];  dX = SiLU' dA_base + sum_c B'_c dA_spline_c
+    SIREN_TRY(kan_gemm(G, out, 1, w.W[l], K, 1, (int)R, (int)K, out, 1, nullptr, w.dA, s));
+    SIREN_TRY(kan_contract(w.X[l], net->grid[l], w.dA, R, in, w.G[cur], s));
+    G = w.G[cur];
+    cur ^= 1;
+  }
+  return SIREN_OK;
+}
+
+}  // extern "C"

@@ -88,6 +88,17 @@ hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_h
 hipError_t col_reduce(const float* part, int64_t row_stride, int nrows, int ncols, float* out,
                       int out_stride, int accumulate, float* tmp, hipStream_t s);
 
+// KAN (kan.hip): fp32, grid_size 5, spline_order 3 (9 A-columns per input)
+hipError_t kan_expand(const float* X, const float* grid, int64_t N, int in, float* A, hipStream_t s);
+hipError_t kan_contract(const float* X, const float* grid, const float* dA, int64_t N, int in, float* dX,
+                        hipStream_t s);
+hipError_t kan_combine(const float* base_w, const float* spline_w, const float* scaler, int out, int in, float* W,
+                       hipStream_t s);
+hipError_t kan_param_grads(const float* dW, const float* spline_w, const float* scaler, int out, int in,
+                           int accumulate, float* g_base, float* g_spline, float* g_scaler, hipStream_t s);
+hipError_t kan_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn, int M,
+                    int N, int64_t K, int splits, float* C, float* out, hipStream_t s);
+
 struct OptState {      // device-resident optimizer + ReduceLROnPlateau state (run.py:116-117)
   double lr;           // current learning rate (param_groups[0]['lr'])
   double best;         // plateau: best loss so far (init +inf)

@@ -26,7 +26,8 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from ._lib import MAX_INNER, ROW_TILE, SirenBatch, SirenGrads, SirenNet, SirenOptState, check, ptr
+from ._lib import (MAX_INNER, ROW_TILE, SirenBatch, SirenGrads, SirenKanBatch, SirenNet, SirenOptState, check,
+                   ptr)
 
 SEG_ALIGN = 64  # floats: every flat segment starts 256-B aligned
 STORE16 = torch.float16  # activation / weight-shadow / dZ storage of the HIP path
@@ -394,3 +395,113 @@ def forward_net(spec: NetSpec, net: SirenNet, coords: torch.Tensor, device, chun
         check(lib.siren_forward(ctypes.byref(net), ctypes.byref(b), s), "siren_forward")
         out[lo:hi] = ws.out[:hi - lo]
     return out
+
+
+def _opt_state_tensor(lr, min_lr, factor, patience, dev) -> torch.Tensor:
+    """siren_opt_state for torch.optim.Adam(lr) + ReduceLROnPlateau(min, factor, patience,
+    min_lr) with torch's defaults (run.py:116-117), as device bytes."""
+    st = SirenOptState()
+    st.lr, st.best, st.step = float(lr), math.inf, 0.0
+    st.num_bad, st.last_epoch = 0, 0
+    st.min_lr, st.factor, st.threshold, st.eps_lr = float(min_lr), float(factor), 1e-4, 1e-8
+    st.patience = int(patience)
+    st.beta1, st.beta2, st.eps = 0.9, 0.999, 1e-8
+    return torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8).to(dev)
+
+
+class KanEngine(SirenEngine):
+    """Full-batch fit of the KAN variant (run.py:92-93 arch='kan') on the HIP
+    path: siren_kan_train_step per micro-batch, gradient all-reduce across DP ranks, then the
+    same flat Adam + ReduceLROnPlateau kernels as the SIREN path.  Shares the optimizer,
+    history, checkpoint and graph-capture methods of SirenEngine."""
+
+    def __init__(self, model, coords: torch.Tensor, target: torch.Tensor, *, lr: float = 1e-3,
+                 min_lr: float = 1e-6, factor: float = 0.8, patience: int = 200,
+                 n_total: int | None = None, micro_batch: int = 1 << 20, hist_cap: int = 20000,
+                 splits: int = 16, device=None):
+        from .kan import make_kan_grads
+        lib = _lib.load()
+        self.lib = lib
+        self.device = dev = torch.device(device or "cuda")
+        if dev.type != "cuda":
+            raise RuntimeError("KanEngine runs on the GPU only (HIP kernels; no CPU fallback)")
+        model.hip_check()
+        self.model = model.to(dev)
+        self.spec = None
+        self.layout = lay = ParamLayout(model)
+        self.params = torch.zeros(lay.flat_len, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for i, (_, p) in enumerate(model.named_parameters()):
+                lay.view(self.params, i).copy_(p.detach().to(dev, torch.float32))
+        d = _dist()
+        if d is not None:
+            d.broadcast(self.params, src=0)
+        for i, (_, p) in enumerate(model.named_parameters()):
+            p.data = lay.view(self.params, i)
+        self.grads = torch.zeros_like(self.params)
+        self.exp_avg = torch.zeros_like(self.params)
+        self.exp_avg_sq = torch.zeros_like(self.params)
+        views = [lay.view(self.params, i) for i in range(len(lay.names))]
+        gviews = [lay.view(self.grads, i) for i in range(len(lay.names))]
+        self.net = model.make_net(views)
+        self.grad_struct = make_kan_grads(model, gviews, self.grads.data_ptr() + 4 * lay.sse_offset,
+                                          self.grads, lay.flat_len)
+        self.state = _opt_state_tensor(lr, min_lr, factor, patience, dev)
+        self.hist_cap = int(hist_cap)
+        self.loss_hist = torch.zeros(max(self.hist_cap, 1), dtype=torch.float32, device=dev)
+        self.lr_hist = torch.zeros(max(self.hist_cap, 1), dtype=torch.float64, device=dev)
+
+        in_dim = model.widths[0]
+        coords = coords.reshape(-1, in_dim).to(torch.float32)
+        target = target.reshape(-1).to(torch.float32)
+        n_global = coords.shape[0] if n_total is None else int(n_total)
+        rank, world = (d.get_rank(), d.get_world_size()) if d is not None else (0, 1)
+        if n_total is None and world > 1:
+            lo, hi = shard_range(n_global, rank, world)
+            coords, target = coords[lo:hi], target[lo:hi]
+        self.n_total = n_global
+        self.n_local = n = coords.shape[0]
+        self.rows = mb = max(1, min(int(micro_batch), n))
+        self.n_micro = max(1, -(-n // mb))
+        self.coords = coords.to(dev).contiguous()
+        self.target = target.to(dev).contiguous()
+        self.splits = int(splits)
+        self.ws = torch.empty(int(lib.siren_kan_workspace_floats(ctypes.byref(self.net), mb, self.splits)),
+                              device=dev)
+        self.out = torch.empty(mb, device=dev)
+        self.g = torch.empty(mb, device=dev)
+        self.batches = []
+        for k in range(self.n_micro):
+            lo = k * mb
+            hi = min(n, lo + mb)
+            b = SirenKanBatch()
+            b.rows, b.n_valid, b.n_total = hi - lo, hi - lo, float(n_global)
+            b.splits, b.zero_grads = self.splits, int(k == 0)
+            b.coords, b.target = self.coords[lo:hi].data_ptr(), self.target[lo:hi].data_ptr()
+            b.out, b.g, b.ws = ptr(self.out), ptr(self.g), ptr(self.ws)
+            self.batches.append(b)
+        self.steps_done = 0
+        self.graph = None
+
+    def _refresh_shadows(self):
+        pass
+
+    def _launch_grads(self):
+        s = self._stream()
+        for b in self.batches:
+            check(self.lib.siren_kan_train_step(ctypes.byref(self.net), ctypes.byref(self.grad_struct),
+                                                ctypes.byref(b), s), "siren_kan_train_step")
+
+    def _launch_update(self):
+        s = self._stream()
+        check(self.lib.siren_adam_step(ptr(self.params), ptr(self.grads), ptr(self.exp_avg), ptr(self.exp_avg_sq),
+                                       self.layout.n_params, ptr(self.state), s), "siren_adam_step")
+        check(self.lib.siren_plateau_step(ptr(self.state), self.grads.data_ptr() + 4 * self.layout.sse_offset,
+                                          float(self.n_total), ptr(self.loss_hist), ptr(self.lr_hist),
+                                          self.hist_cap, s), "siren_plateau_step")
+
+    @torch.no_grad()
+    def infer(self, coords: torch.Tensor, chunk: int | None = None) -> torch.Tensor:
+        from .kan import kan_forward
+        return kan_forward(self.model, coords.reshape(-1, self.model.widths[0]), self.device,
+                           chunk or self.rows, net=self.net)

@@ -3,7 +3,8 @@
 Differences from the reference are limited to what the hot-path scope excludes: no plots
 (matplotlib figures), no loss-landscape, no STFT/MAE/SNR loss mixes (alpha must be 0 and
 loss_mode 'mse' -- at alpha=0 the reference's STFT term contributes exactly zero, SURVEY
-§8 a8), no random-Fourier-feature encoding, no KAN.  method='mdct' fits the
+§8 a8), no random-Fourier-feature encoding.  arch='kan' fits KAN([1, H, H, 1]) (SURVEY §8 f4,
+kan.py) on its own fp32 HIP kernels.  method='mdct' fits the
 MDCT-domain target (utils.MDCTFitting, N = 2048, mode='log' = takelog) with
 (bin, frame) coordinates and inverts it as run.py:258-290 does.  Everything the path
 produces -- output.wav, the checkpoint dict, parameters.json with the run.py-formula SNR --
@@ -22,7 +23,8 @@ import numpy as np
 import scipy.io.wavfile as wavfile
 import torch
 
-from .engine import SirenEngine
+from .engine import KanEngine, SirenEngine
+from .kan import KAN
 from .models import SirenWithSnakeTanh
 from .utils import (MDCTFitting, WaveformFitting, calculate_snr, get_coord, load_mono_like_librosa,
                     reported_snr)
@@ -54,8 +56,10 @@ def train(experiment_path: str, tag: str, inst: str, duration: int, num_channels
         raise ValueError("specify the correct fitting method as wave or mdct (run.py:77-78)")
     if method == "mdct" and bwe:
         raise NotImplementedError("bwe is a waveform-mode feature (run.py:127-131)")
-    if arch != "mlp":
-        raise NotImplementedError("arch='kan' is SURVEY §8 f4 (not on the HIP path yet)")
+    if arch not in ("mlp", "kan"):
+        raise NotImplementedError(f"arch={arch!r}: the reference builds 'kan' or the MLP (run.py:92-96)")
+    if arch == "kan" and method == "mdct":
+        raise NotImplementedError("arch='kan' takes 1-D coordinates (run.py:92 builds KAN([1, H, H, 1]))")
     if loss_mode != "mse" or alpha != 0.0:
         raise NotImplementedError("HIP path implements loss_mode='mse' with alpha=0 (run.py:167-169)")
     if num_freq is not None:
@@ -88,19 +92,23 @@ def train(experiment_path: str, tag: str, inst: str, duration: int, num_channels
 
     if seed is not None:
         torch.manual_seed(seed)
-    model = SirenWithSnakeTanh(in_features=input_dimension, out_features=1,
-                               hidden_features=num_hidden_features, num_sine=num_sine,
-                               num_snake=num_snake, num_tanh=num_tanh, num_freq=num_freq,
-                               first_linear=first_linear, last_linear=last_linear,
-                               first_omega_0=omega, hidden_omega_0=hidden_omega, a_initial=a_initial)
+    if arch == "kan":  # run.py:92-93
+        model = KAN([1, num_hidden_features, num_hidden_features, 1])
+    else:
+        model = SirenWithSnakeTanh(in_features=input_dimension, out_features=1,
+                                   hidden_features=num_hidden_features, num_sine=num_sine,
+                                   num_snake=num_snake, num_tanh=num_tanh, num_freq=num_freq,
+                                   first_linear=first_linear, last_linear=last_linear,
+                                   first_omega_0=omega, hidden_omega_0=hidden_omega, a_initial=a_initial)
     ckpt = None
     if prev_ckpt_path is not None:  # run.py:84-106
         ckpt = torch.load(prev_ckpt_path, map_location="cpu", weights_only=True)
         model.load_state_dict(ckpt["model_state_dict"])
 
     dev = torch.device(device or "cuda")
-    engine = SirenEngine(model, model_input, ground_truth, lr=learning_rate, min_lr=min_learning_rate,
-                         micro_batch=micro_batch, hist_cap=total_steps, device=dev)
+    Engine = KanEngine if arch == "kan" else SirenEngine
+    engine = Engine(model, model_input, ground_truth, lr=learning_rate, min_lr=min_learning_rate,
+                    micro_batch=micro_batch, hist_cap=total_steps, device=dev)
     if ckpt is not None:
         engine.load_adam_state_dict(ckpt["optimizer_state_dict"])
 

@@ -336,3 +336,68 @@ def fit(p: Params, t, y, omega0, omega, steps, lr=1e-3, min_lr=1e-6, half=False)
         losses.append(float(loss))
         lrs.append(sched.step(loss))
     return Params.from_state_dict(dict(zip(names, flat)), *counts), np.array(losses), np.array(lrs)
+
+
+# ------------------------------------------------------------------ KAN variant (kan.py)
+def kan_bases(x: np.ndarray, knots: np.ndarray, order: int = 3, deriv: bool = False):
+    """Cox-de Boor bases of kan.py:94-104 in fp32 (same op order), x [N][in], knots [in][G]
+    -> [N][in][G-1-order]; with deriv also d bases / dx (the recursion differentiated)."""
+    x = np.asarray(x, F32)[:, :, None]
+    g = np.asarray(knots, F32)[None]
+    b = ((x >= g[..., :-1]) & (x < g[..., 1:])).astype(F32)
+    db = np.zeros_like(b)
+    for k in range(1, order + 1):
+        dl = (g[..., k:-1] - g[..., :-(k + 1)]).astype(F32)
+        dr = (g[..., k + 1:] - g[..., 1:(-k)]).astype(F32)
+        left = ((x - g[..., :-(k + 1)]) / dl).astype(F32)
+        right = ((g[..., k + 1:] - x) / dr).astype(F32)
+        if deriv:
+            db = (b[..., :-1] / dl + left * db[..., :-1] - b[..., 1:] / dr + right * db[..., 1:]).astype(F32)
+        b = (left * b[..., :-1] + right * b[..., 1:]).astype(F32)
+    return (b, db) if deriv else b
+
+
+def kan_forward(sd: dict, x: np.ndarray, n_layers: int, dtype=F64):
+    """KAN forward (kan.py:153-166) from a state_dict: per layer A = [SiLU(x) | bases(x)],
+    out = A [base_w | spline_w * scaler]^T.  Returns (out [N], cache of per-layer inputs)."""
+    xs = [np.asarray(x, F32).reshape(x.shape[0], -1)]
+    for l in range(n_layers):
+        pre = f"layers.{l}."
+        xin = xs[-1]
+        bw = np.asarray(sd[pre + "base_weight"], dtype)
+        sw = np.asarray(sd[pre + "spline_weight"], dtype) * np.asarray(sd[pre + "spline_scaler"], dtype)[..., None]
+        xd = xin.astype(dtype)
+        silu = xd / (1 + np.exp(-xd))
+        bases = kan_bases(xin, sd[pre + "grid"]).astype(dtype)
+        out = silu @ bw.T + bases.reshape(xin.shape[0], -1) @ sw.reshape(sw.shape[0], -1).T
+        xs.append(out.astype(F32) if dtype == F32 else out)
+    return np.asarray(xs[-1]).reshape(-1), xs
+
+
+def kan_backward(sd: dict, xs: list, g: np.ndarray, n_layers: int) -> dict:
+    """Autograd of kan_forward for dLoss/dout = g [N] (fp64): grads of base_weight,
+    spline_weight (x scaler) and spline_scaler (sum_c dW * spline_weight) per layer."""
+    grads = {}
+    G = np.asarray(g, F64).reshape(-1, 1)
+    for l in range(n_layers - 1, -1, -1):
+        pre = f"layers.{l}."
+        xin = xs[l]
+        xd = np.asarray(xin, F64)
+        s = 1 / (1 + np.exp(-xd))
+        silu, dsilu = xd * s, s * (1 + xd * (1 - s))
+        b, db = kan_bases(np.asarray(xin, F32), sd[pre + "grid"], deriv=True)
+        b, db = b.astype(F64), db.astype(F64)
+        n, i = xin.shape
+        bw = np.asarray(sd[pre + "base_weight"], F64)
+        spw = np.asarray(sd[pre + "spline_weight"], F64)
+        scl = np.asarray(sd[pre + "spline_scaler"], F64)
+        dS = (G.T @ b.reshape(n, -1)).reshape(spw.shape)
+        grads[pre + "base_weight"] = G.T @ silu
+        grads[pre + "spline_weight"] = dS * scl[..., None]
+        grads[pre + "spline_scaler"] = (dS * spw).sum(-1)
+        if l > 0:
+            sw = spw * scl[..., None]
+            dA_base = G @ bw
+            dA_spl = (G @ sw.reshape(sw.shape[0], -1)).reshape(n, i, -1)
+            G = dsilu * dA_base + (db * dA_spl).sum(-1)
+    return grads

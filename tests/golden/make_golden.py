@@ -188,6 +188,36 @@ def mdct_fixtures(ref_models, steps):
         print(f"mdct 5x512: losses {losses[:3]} ... {losses[-1]:.3e}", flush=True)
 
 
+def kan_fixtures(ref_utils, steps):
+    """KAN variant (kan.py, run.py:92-93): init state_dicts (with the grid
+    buffers), one forward/backward on the 2100-point gt_bach subset, and a short full-batch
+    trajectory of KAN([1, 64, 64, 1]) on gt_bach 1 s."""
+    import kan as ref_kan  # noqa: E402  (the reference's own module)
+    wav = os.path.join(REF, "gt_bach.wav")
+    coords, target = ref_utils.WaveformFitting(wav, duration=1, decimation=1)[0]
+    idx = np.arange(0, 44100, 21)
+    fb = {"subset_idx": idx}
+    for name, widths, seed in (("k64", [1, 64, 64, 1], 0), ("k128", [1, 128, 128, 1], 3)):
+        torch.manual_seed(seed)
+        m = ref_kan.KAN(widths)
+        for k, v in sd_np(m).items():
+            fb[f"{name}_init_{k}"] = v
+        if name == "k64":
+            out, loss, grads = fwd_bwd(m, coords[idx], target[idx])
+            fb[f"{name}_out"] = out
+            fb[f"{name}_loss"] = np.array([loss])
+            for k, gr in grads.items():
+                fb[f"{name}_grad_{k}"] = gr
+    np.savez_compressed(os.path.join(OUT, "kan_fwd_bwd.npz"), **fb)
+    if steps > 0:
+        torch.manual_seed(0)
+        m = ref_kan.KAN([1, 64, 64, 1])
+        losses, lrs, _ = restated_loop(m, coords, target, steps)
+        json.dump({"steps": steps, "widths": [1, 64, 64, 1], "seed": 0, "loss": losses.tolist(), "lr": lrs.tolist()},
+                  open(os.path.join(OUT, "trajectory_kan_64.json"), "w"))
+        print(f"kan: losses {losses[:3]} ... {losses[-1]:.3e}", flush=True)
+
+
 def snake_seed_trajectories(ref_models, ref_utils, seeds, steps):
     """train()'s default architecture (num_sine=2, num_snake=2, a_initial=0.5, H=256,
     omega0=1000) over several init seeds: loss / lr traces for the multi-seed fit protocol."""
@@ -233,11 +263,15 @@ def main():
     ap.add_argument("--only-act", action="store_true", help="write only the Snake / Tanh fixtures")
     ap.add_argument("--snake-seeds", default="", help="write only the Snake multi-seed trajectories")
     ap.add_argument("--only-mdct", action="store_true", help="write only the MDCT fixtures")
+    ap.add_argument("--only-kan", action="store_true", help="write only the KAN fixtures")
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 1)
     ref_models, ref_utils = import_reference()
     if args.only_act:
         act_fixtures(ref_models, ref_utils, args.trajectory_steps)
+        return
+    if args.only_kan:
+        kan_fixtures(ref_utils, args.trajectory_steps)
         return
     if args.only_mdct:
         mdct_fixtures(ref_models, args.trajectory_steps)
@@ -346,6 +380,7 @@ def main():
                           args.trajectory_steps)
     act_fixtures(ref_models, ref_utils, args.trajectory_steps)
     mdct_fixtures(ref_models, 20)
+    kan_fixtures(ref_utils, 30)
     json.dump(meta, open(os.path.join(OUT, "meta.json"), "w"), indent=1)
     print("golden fixtures written to", OUT)
 

@@ -137,7 +137,8 @@ def test_waveform_fitting_and_reported_snr(tmp_path):
 
 def test_unsupported_train_options_raise(tmp_path):
     from inr_for_audio_amd.run import train
-    for kw in (dict(method="mdct", bwe=True), dict(arch="kan"), dict(loss_mode="mae"), dict(alpha=0.5)):
+    for kw in (dict(method="mdct", bwe=True), dict(arch="kan", method="mdct"), dict(arch="rbf"),
+               dict(loss_mode="mae"), dict(alpha=0.5)):
         with pytest.raises(NotImplementedError):
             train(str(tmp_path), "t", "x", 1, **kw)
     with pytest.raises(ValueError):
