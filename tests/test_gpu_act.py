@@ -274,23 +274,31 @@ def test_fit_default_snake_first_steps_track_reference(dev):
 
 
 def test_fit_default_snake_quality_over_seeds(dev):
-    """Multi-seed fit protocol of tests/test_gpu_fit.py on the Snake default architecture:
-    median over init seeds of the best-loss SNR within 0.5 dB of the reference's runs of the
-    same seeds (tests/golden/trajectory_snake_default_seeds.json)."""
+    """Multi-seed fit protocol of tests/test_gpu_fit.py on the Snake default architecture, vs
+    the reference's runs of the same seeds (tests/golden/trajectory_snake_default_seeds.json):
+    the median over seeds of the best-loss SNR within 0.5 dB.  At lr 1e-3 this architecture
+    spends ~40 % of its 300 steps inside Adam loss spikes (loss > 10x the running minimum) --
+    the reference itself ends 3 of 8 seeds at ~0 dB -- so the final SNR is a coin flip per
+    seed; the spike rate summed over seeds is compared instead (within a factor 1.5)."""
     ref = json.load(open(os.path.join(GOLDEN, "trajectory_snake_default_seeds.json")))
     var = float(np.mean(np.load(os.path.join(GOLDEN, "gt_bach_1s.npz"))["target"].astype(np.float64) ** 2))
-    best_gpu, best_ref, fin_gpu, fin_ref = [], [], [], []
+
+    def spikes(x):
+        x = np.asarray(x)
+        return int(np.sum(x > 10 * np.minimum.accumulate(x)))
+
+    best_gpu, best_ref, sp_gpu, sp_ref = [], [], 0, 0
     for s in sorted(int(k) for k in ref["runs"]):
-        eng, snr = _fit_snake(dev, ref["steps"], s)
+        eng, _ = _fit_snake(dev, ref["steps"], s)
         losses, _ = eng.history()
         r = ref["runs"][str(s)]
         best_gpu.append(10 * np.log10(var / float(np.min(losses))))
         best_ref.append(10 * np.log10(var / float(np.min(r["loss"]))))
-        fin_gpu.append(snr)
-        fin_ref.append(r["snr_target"])
+        sp_gpu += spikes(losses)
+        sp_ref += spikes(r["loss"])
     med = lambda x: float(np.median(x))  # noqa: E731
     print(f"\nSnake default best-loss SNR median: GPU {med(best_gpu):.2f} dB, reference {med(best_ref):.2f} dB"
-          f"\nfinal SNR median: GPU {med(fin_gpu):.2f} dB, reference {med(fin_ref):.2f} dB"
+          f"\nspike steps: GPU {sp_gpu}, reference {sp_ref}"
           f"\nper seed GPU best {np.round(best_gpu, 2).tolist()}\nper seed ref best {np.round(best_ref, 2).tolist()}")
     assert abs(med(best_gpu) - med(best_ref)) < 0.5
-    assert abs(med(fin_gpu) - med(fin_ref)) < 6.0
+    assert sp_ref / 1.5 <= sp_gpu <= sp_ref * 1.5
