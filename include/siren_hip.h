@@ -108,6 +108,12 @@ typedef struct siren_batch {
   float* slab;           /* [splits][H][H]                                      */
   uint16_t* E[SIREN_MAX_INNER + 1];  /* E[i+1] fp16 [rows][H]: dY/da of Snake inner layer
                                         i (NULL for other layers)                      */
+  /* optional gradient-ready events (hipEvent_t, NULL = none), recorded on `stream` as soon
+   * as a bucket's gradients are final in this call -- set them on the LAST micro-batch so a
+   * data-parallel caller can all-reduce each bucket on a communication stream while the rest
+   * of the backward runs.  [i < L]: inner layer i (W_i, b_i, Snake a_i);
+   * [L]: the first layer (W0, b0); [L+1]: the head (w_head, b_head) and `sse`. */
+  void* grad_ready[SIREN_MAX_INNER + 2];
 } siren_batch;
 
 /* Workspace sizing / tiling helpers.  siren_nt_tile: tile edge the NT GEMMs use for
@@ -265,7 +271,8 @@ enum siren_prof_kind {
  * SIREN_OPT_NT_PIPE = 256x256 NT GEMM variant: -1 per mode (default: 4 for the forward, 1 for
  * dX), 0 BK 64 one tile per block, 1 BK 64 persistent, 2 BK 32 4-slot ring persistent, 3 BK 32 3-slot ring persistent,
  * 4 BK 64 persistent with two wave groups in ping-pong, 5 BK 64 persistent with the X operand
- * prefetched into L2 SIREN_OPT_NT_PF_DIST (1..16, default 2) K-steps ahead;
+ * prefetched into L2 SIREN_OPT_NT_PF_DIST (1..16, default 2) K-steps ahead, 6 / 7 128x256 tiles
+ * (4 waves), BK 32 3- / 2-slot ring, persistent with two blocks per CU;
  * SIREN_OPT_TN_PIPE = 0..3 selects the 256x256 dW K-loop (0: BK 64 double buffer
  * (default), 1: BK 32 4-slot ring, 2: BK 32 5-slot ring, 3: BK 64 ping-pong);
  * SIREN_OPT_NT_GRID = persistent NT grid size (0 = one block per CU; tests use small

@@ -66,6 +66,7 @@ class SirenBatch(ctypes.Structure):
         ("out", _p), ("g", _p), ("head_part", _p), ("sse_part", _p), ("gsum_part", _p),
         ("gmax_part", _p), ("gscale", _p), ("col_part", _p), ("col_part2", _p), ("red_tmp", _p), ("slab", _p),
         ("E", _p * (MAX_INNER + 1)),
+        ("grad_ready", _p * (MAX_INNER + 2)),
     ]
 
 

@@ -92,6 +92,11 @@ int check_batch(const siren_net* n, const siren_batch* b, bool train) {
   return SIREN_OK;
 }
 
+// record batch->grad_ready[k] (if set) on the stream
+inline hipError_t mark_ready(const siren_batch* b, int k, hipStream_t s) {
+  return b->grad_ready[k] ? hipEventRecord((hipEvent_t)b->grad_ready[k], s) : hipSuccess;
+}
+
 // forward through all layers + head partials; returns hip status
 hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s) {
   const int R = b->rows, H = n->hidden, L = n->n_inner;
@@ -191,6 +196,7 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
   SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, R / 128, H, gr->b[L - 1], 1, 1, b->red_tmp, s));
   if (snake_last)
     SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(da_last, H, R / 128, H, gr->a[L - 1], 1, 1, b->red_tmp, s));
+  SIREN_TRY(mark_ready(b, L + 1, s));  // head: w_head, b_head (and sse, summed before the backward)
 
   int cur = 0;
   for (int i = L - 1; i >= 0; --i) {
@@ -204,6 +210,7 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
     SIREN_PROF(SIREN_PROF_BWD_DW, s, gemm_tn_dw(tp, s));
     SIREN_PROF(SIREN_PROF_REDUCE, s, dw_reduce(b->slab, b->splits, H, H, tntile, gr->W[i], 1,
                                                        b->gscale, s));
+    SIREN_TRY(mark_ready(b, i, s));  // W_i now; b_i and a_i were reduced one stage earlier
 
     NtParams p = {};
     p.X = B(b->dZ[cur]);
@@ -236,6 +243,7 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
       for (int j = 0; j < in; ++j)
         SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + (int64_t)(1 + j) * H, rs, prow, H,
                                                     gr->W0 + j, in, 1, b->red_tmp, s));
+      SIREN_TRY(mark_ready(b, L, s));
     }
   }
   return SIREN_OK;
@@ -471,7 +479,7 @@ int siren_set_option(int32_t option, int32_t value) {
       return SIREN_OK;
     case SIREN_OPT_NT_PIPE:
     case SIREN_OPT_TN_PIPE:
-      if (value < (option == SIREN_OPT_NT_PIPE ? -1 : 0) || value > (option == SIREN_OPT_NT_PIPE ? 5 : 3))
+      if (value < (option == SIREN_OPT_NT_PIPE ? -1 : 0) || value > (option == SIREN_OPT_NT_PIPE ? 7 : 3))
         return SIREN_ERR_CONFIG;
       if (option == SIREN_OPT_NT_PIPE) gemm_nt_set_pipe(value);
       else gemm_tn_set_pipe(value);

@@ -47,9 +47,11 @@ __device__ __forceinline__ int stage_swz(int r, int c) {
   else return c ^ ((0x78 >> (2 * ((r >> 2) & 3))) & 3);  // H as 2-bit fields of 0x78
 }
 
-template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_, bool PP_ = false, int PF_ = 0>
+template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_, bool PP_ = false, int PF_ = 0, int BPC_ = 1>
 struct NtCfg {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, S = S_;
+  static constexpr int BPC = BPC_;  // persistent grid: blocks per CU (2: two independent tile
+                                    // streams per CU, one's epilogue under the other's MFMAs)
   static constexpr bool PP = PP_;  // ping-pong K-loop (gemm_pipeline.h pingpong_tiles)
   // L2 prefetch of the X operand p.pf_dist K-steps ahead of the LDS-DMA: one 4-B touch per
   // 128-B line, PF instructions per wave per stage (BM*BK*2/128 lines over the block)
@@ -66,15 +68,12 @@ struct NtCfg {
   // then (NT_FWD) the whole bias and head weight vectors, staged once per block
   static constexpr int RED = 4 * (WN * BM > 3 * WM * BN ? WN * BM : 3 * WM * BN);
   static constexpr int MAXN = 1024;
-  static constexpr int PFLDS = RING + RED + 2 * 4 * MAXN;  // 256-B prefetch landing area
-  static constexpr int ALDS = PFLDS + (PF ? 256 : 0);      // NT_FWD_SNAKE: a
-  static constexpr int LDS = ALDS;
-  static constexpr int LDS_SNAKE = ALDS + 4 * MAXN;
+  static constexpr int VEC = 4 * MAXN;  // one per-column fp32 vector
   static constexpr int XINSTR = XBYTES / 1024 / NWAVES;  // LDS-DMA instructions per wave per stage
   static constexpr int WINSTR = WBYTES / 1024 / NWAVES;
   static_assert(XBYTES % (1024 * NWAVES) == 0 && WBYTES % (1024 * NWAVES) == 0, "staging split");
   static_assert(SN % 2 == 0, "16-B row pieces pair adjacent column subtiles");
-  static_assert(LDS_SNAKE <= 160 * 1024, "LDS");
+  static_assert(RING + RED + 3 * VEC + 256 <= 160 * 1024, "LDS");
 };
 using NtSmall = NtCfg<128, 128, 2, 2, 64, 2>;
 // 256x256 variants (siren_set_option SIREN_OPT_NT_PIPE): BK 64 double buffer (one tile per
@@ -86,6 +85,23 @@ using NtLargeR3 = NtCfg<256, 256, 2, 4, 32, 3>;
 using NtLargePP = NtCfg<256, 256, 2, 4, 64, 2, true>;
 // BK 64 double buffer, persistent, X prefetched into L2 ahead of the LDS-DMA (NT_PIPE 5)
 using NtLargePF = NtCfg<256, 256, 2, 4, 64, 2, false, 1>;
+// 128x256 tiles, 4 waves (1x4, 128x64 each), BK 32 3-slot ring, persistent with TWO blocks
+// per CU (NT_PIPE 6) / BK 32 double buffer (NT_PIPE 7)
+using NtMid3 = NtCfg<128, 256, 1, 4, 32, 3, false, 0, 2>;
+using NtMid2 = NtCfg<128, 256, 1, 4, 32, 2, false, 0, 2>;
+
+// LDS layout of one kernel instance: the ring, the epilogue reduction scratch, then only the
+// per-column vectors its mode needs (bias for the forward modes, head weights with HEAD, Snake
+// a), then the prefetch landing area -- so DX kernels and head-less forwards stay small enough
+// for two blocks per CU where the config asks for it.
+template <class Cfg, int MODE, bool HEAD>
+struct NtLds {
+  static constexpr int BIAS = Cfg::RING + Cfg::RED;
+  static constexpr int HW = BIAS + (nt_is_fwd(MODE) ? Cfg::VEC : 0);
+  static constexpr int A = HW + (HEAD ? Cfg::VEC : 0);
+  static constexpr int PF = A + (MODE == NT_FWD_SNAKE ? Cfg::VEC : 0);
+  static constexpr int SIZE = PF + (Cfg::PF ? 256 : 0);
+};
 
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
@@ -100,7 +116,8 @@ template <class Cfg, int MODE, bool HEAD>
 __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, BK = Cfg::BK, WN = Cfg::WN;
   constexpr int TM = Cfg::TM, TN = Cfg::TN, SM = Cfg::SM, SN = Cfg::SN;
-  __shared__ __attribute__((aligned(16))) char smem[MODE == NT_FWD_SNAKE ? Cfg::LDS_SNAKE : Cfg::LDS];
+  using Lay = NtLds<Cfg, MODE, HEAD>;
+  __shared__ __attribute__((aligned(16))) char smem[Lay::SIZE];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -165,7 +182,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
       for (int j = 0; j < Cfg::PF; ++j) {
         const int r = (wave * Cfg::PF + j) * 32 + (lane & 31);
-        gpf4_asm(p.X + (size_t)(pm0 + r) * K + pk * BK + (lane >> 5) * 32, lds_addr(smem + Cfg::PFLDS));
+        gpf4_asm(p.X + (size_t)(pm0 + r) * K + pk * BK + (lane >> 5) * 32, lds_addr(smem + Lay::PF));
       }
     }
   };
@@ -206,9 +223,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
-  float* bias_lds = (float*)(smem + Cfg::RING + Cfg::RED);
-  float* hw_lds = bias_lds + Cfg::MAXN;
-  float* a_lds = (float*)(smem + Cfg::ALDS);  // Snake: a
+  float* bias_lds = (float*)(smem + Lay::BIAS);
+  float* hw_lds = (float*)(smem + Lay::HW);
+  float* a_lds = (float*)(smem + Lay::A);  // Snake: a
   if constexpr (nt_is_fwd(MODE)) {
     for (int c = tid * 4; c < N; c += Cfg::THREADS * 4) {
       *(float4*)(bias_lds + c) = *(const float4*)(p.bias + c);
@@ -531,7 +548,7 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
         g_num_cus <= 0)
       g_num_cus = 256;
   }
-  const int cap = g_nt_grid_cap > 0 ? g_nt_grid_cap : g_num_cus;
+  const int cap = g_nt_grid_cap > 0 ? g_nt_grid_cap : g_num_cus * Cfg::BPC;
   const int grid = persistent ? (ntiles < cap ? ntiles : cap) : ntiles;
   hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD>), dim3(grid), dim3(Cfg::THREADS), 0, s, p);
   return hipGetLastError();
@@ -602,6 +619,8 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
       case 3: return dispatch_mode<NtLargeR3>(mode, head, p, s, true);
       case 4: return dispatch_mode<NtLargePP>(mode, head, p, s, true);
       case 5: return dispatch_mode<NtLargePF>(mode, head, p, s, true);
+      case 6: return dispatch_mode<NtMid3>(mode, head, p, s, true);
+      case 7: return dispatch_mode<NtMid2>(mode, head, p, s, true);
       default: return dispatch_mode<NtLarge>(mode, head, p, s, true);
     }
   }

@@ -187,7 +187,13 @@ def shard_range(n_total: int, rank: int, world: int) -> tuple[int, int]:
 
 
 class SirenEngine:
-    """Full-batch SIREN fit on one GPU (or one DP rank): run.py:108-190 minus the plots."""
+    """Full-batch SIREN fit on one GPU (or one DP rank): run.py:108-190 minus the plots.
+
+    Data parallel (torch.distributed initialised, world > 1): the gradients are all-reduced in
+    per-layer buckets on a communication stream, each as soon as the backward has finalised it
+    (siren_batch.grad_ready events), so RCCL runs under the remaining backward GEMMs."""
+
+    _buckets = None  # [(event index, lo, hi)] in completion order (DP only)
 
     def __init__(self, model, coords: torch.Tensor, target: torch.Tensor, *, lr: float = 1e-3,
                  min_lr: float = 1e-6, factor: float = 0.8, patience: int = 200,
@@ -269,7 +275,30 @@ class SirenEngine:
             self.batches.append(self.ws.batch(c, t, min(mb, n - lo), n_global, zero_grads=(k == 0)))
         self.steps_done = 0
         self.graph = None
+        if d is not None:
+            self._setup_buckets()
         self._refresh_shadows()
+
+    def _setup_buckets(self):
+        """One bucket per layer (contiguous in the flat layout): the head (+ the SSE tail slot),
+        inner layers L-1 .. 0, then the first layer -- the order the backward finalises them."""
+        lay, ix, L = self.layout, self.ix, self.spec.n_inner
+        span = lambda ids: (lay.offsets[min(ids)], lay.offsets[max(ids)] + lay.numels[max(ids)])  # noqa: E731
+        order = [(L + 1, lay.offsets[ix["wh"]], lay.flat_len)]
+        for i in range(L - 1, -1, -1):
+            ids = [ix["W"][i], ix["b"][i]] + ([ix["a"][i]] if ix["a"][i] is not None else [])
+            order.append((i,) + span(ids))
+        order.append((L,) + span([ix["W0"], ix["b0"]]))
+        self._events = []
+        for _ in range(L + 2):
+            ev = torch.cuda.Event()
+            ev.record()  # materialise the hipEvent_t so its handle can go to the C-ABI
+            self._events.append(ev)
+        last = self.batches[-1]
+        for k, ev in enumerate(self._events):
+            last.grad_ready[k] = ev.cuda_event
+        self._comm = torch.cuda.Stream(self.device)
+        self._buckets = order
 
     # ------------------------------------------------------------------ internals
     def _stream(self) -> int:
@@ -300,7 +329,17 @@ class SirenEngine:
         else:
             self._launch_grads()
             d = _dist()
-            if d is not None:
+            if d is not None and self._buckets is not None:
+                # bucket k goes out as soon as the backward recorded grad_ready[k]
+                works = []
+                with torch.cuda.stream(self._comm):
+                    for k, lo, hi in self._buckets:
+                        self._comm.wait_event(self._events[k])
+                        works.append(d.all_reduce(self.grads[lo:hi], async_op=True))
+                for w in works:
+                    w.wait()
+                torch.cuda.current_stream(self.device).wait_stream(self._comm)
+            elif d is not None:
                 d.all_reduce(self.grads)
             self._launch_update()
         self.steps_done += 1

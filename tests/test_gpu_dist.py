@@ -21,25 +21,30 @@ def _free_port():
     return p
 
 
-def _setup():
+CFGS = {"sine": ((2, 0, 0), 1 << 20), "snake_mb": ((2, 2, 0), 1024)}
+
+
+def _setup(cfg="sine"):
     import sys
     sys.path.insert(0, ROOT)
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     torch.manual_seed(0)
-    m = SirenWithSnakeTanh(1, 1, 256, 2, 0, 0, first_omega_0=2000.0, hidden_omega_0=30.0)
+    (ns, nk, nt), _ = CFGS[cfg]
+    m = SirenWithSnakeTanh(1, 1, 256, ns, nk, nt, first_omega_0=2000.0, hidden_omega_0=30.0, a_initial=0.5)
     n = 5001
     t = torch.linspace(-1, 1, n).reshape(n, 1)
     y = 0.5 * torch.sin(37 * t) + 0.2 * torch.sin(91 * t)
     return m, t, y
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, cfg):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from inr_for_audio_amd.engine import SirenEngine
-    m, t, y = _setup()
-    eng = SirenEngine(m, t, y, device=torch.device("cuda:0"))
+    m, t, y = _setup(cfg)
+    eng = SirenEngine(m, t, y, micro_batch=CFGS[cfg][1], device=torch.device("cuda:0"))
+    assert eng._buckets is not None and eng.n_micro == (1 if cfg == "sine" else 3)
     eng.step()
     g1 = eng.grads.cpu().numpy().copy()
     eng.step()
@@ -48,19 +53,22 @@ def _rank(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_engine_matches_single(lib):
+@pytest.mark.parametrize("cfg", list(CFGS))
+def test_two_rank_engine_matches_single(lib, cfg):
+    """Per-layer gradient buckets all-reduced on a communication stream as the backward
+    finalises them (grad_ready events on the last micro-batch) == one full-batch step."""
     from inr_for_audio_amd.engine import SirenEngine
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, cfg)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r[0], r[1:]) for r in (q.get(timeout=300) for _ in range(2)))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    m, t, y = _setup()
+    m, t, y = _setup(cfg)
     eng = SirenEngine(m, t, y, device=torch.device("cuda:0"))
     eng.step()
     g_full = eng.grads.cpu().numpy().copy()

@@ -51,7 +51,8 @@ def _release():
 
 
 @pytest.fixture(params=[(128, 0, 0), (256, 0, 0), (256, 1, 0), (256, 1, 2), (256, 2, 0), (256, 2, 2),
-                        (256, 3, 3), (256, 4, 0), (256, 4, 2), (256, 4, 3), (256, 5, 0), (256, 5, 3)],
+                        (256, 3, 3), (256, 4, 0), (256, 4, 2), (256, 4, 3), (256, 5, 0), (256, 5, 3),
+                        (256, 6, 0), (256, 6, 3), (256, 7, 0), (256, 7, 5)],
                 ids=lambda p: f"t{p[0]}p{p[1]}g{p[2]}")
 def nt_tile(request, lib):
     """Force the NT GEMM tile edge, persistence and persistent grid size (siren_set_option)
