@@ -48,16 +48,11 @@ hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, 
 // adds < 2e-4 rev with 2^-24 relative error, so r is within ~4e-8 rev (2.5e-7 rad) of a/(2pi)
 // mod 1 for every |a| < 2^17.  v_sin_f32 / v_cos_f32 take revolutions directly.  (OCML's
 // sincosf with its large-argument reduction made this kernel VALU-bound at 2.1 ms.)
-__device__ __forceinline__ void sincos_rev(float a, float* s, float* c) {
-  constexpr float kHi = 0x1.45f306p-3f;  // fp32(1/(2*pi))             0x3E22F983
-  constexpr float kLo = 0x1.b93910p-28f; // fp32(1/(2*pi) - kHi) = 6.42e-9  0x31DC9C88
-  const float n = __builtin_rintf(a * kHi);
-  const float r = __builtin_fmaf(a, kLo, __builtin_fmaf(a, kHi, -n));
-  *s = __builtin_amdgcn_sinf(r);
-  *c = __builtin_amdgcn_cosf(r);
-}
+// (sincos_rev / first_preact live in siren_common.h: the dX GEMM's NT_DX0R epilogue
+// recomputes the same cosine.)
 // Row-wise: each thread owns 8 columns (W0 / b0 in registers) and walks rows; a row is H/8
 // threads, a 256-thread block covers 256/(H/8) rows per pass; Y0 / C0 go out as 16-B pieces.
+template <bool STORE_C>
 __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const float* __restrict__ W0,
                                  const float* __restrict__ b0, float omega0, int R, int H,
                                  h16* __restrict__ Y0, h16* __restrict__ C0) {
@@ -78,9 +73,7 @@ __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const 
     float y[8], c[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const float z = (in_dim == 1) ? __builtin_fmaf(t0, w0[r], bb[r])
-                                    : __builtin_fmaf(t1, w1[r], t0 * w0[r]) + bb[r];
-      sincos_rev(omega0 * z, &y[r], &c[r]);
+      sincos_rev(omega0 * first_preact(in_dim, t0, t1, w0[r], w1[r], bb[r]), &y[r], &c[r]);
     }
     h16x8 yv, cv;
 #pragma unroll
@@ -89,7 +82,7 @@ __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const 
       cv[r] = (h16)c[r];
     }
     *(h16x8*)(Y0 + m * H + n) = yv;
-    *(h16x8*)(C0 + m * H + n) = cv;
+    if constexpr (STORE_C) *(h16x8*)(C0 + m * H + n) = cv;
   }
 }
 
@@ -97,8 +90,13 @@ hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b
                      int R, int H, h16* Y0, h16* C0, hipStream_t s) {
   if (H % 8 || H > 2048 || 256 % (H / 8) || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
   const int rpb = 256 / (H / 8);
-  hipLaunchKernelGGL(first_fwd_kernel, dim3(grid_for(R, rpb, 4096)), dim3(256), 0, s, t, in_dim, W0, b0,
-                     omega0, R, H, Y0, C0);
+  // C0 == NULL: the fused train step recomputes cos in the layer-0 dX epilogue (NT_DX0R)
+  if (C0)
+    hipLaunchKernelGGL(first_fwd_kernel<true>, dim3(grid_for(R, rpb, 4096)), dim3(256), 0, s, t, in_dim, W0, b0,
+                       omega0, R, H, Y0, C0);
+  else
+    hipLaunchKernelGGL(first_fwd_kernel<false>, dim3(grid_for(R, rpb, 4096)), dim3(256), 0, s, t, in_dim, W0, b0,
+                       omega0, R, H, Y0, C0);
   return hipGetLastError();
 }
 

@@ -73,6 +73,29 @@ __device__ __forceinline__ void gpf4_asm(const void* gsrc, unsigned lds_byte) {
       : "memory");
 }
 
+// First SineLayer pre-activation z = t W0^T + b0 rounded as torch's CPU addmm (K=1: one fma;
+// K=2: fma(t1, w1, t0*w0) + b) -- models.py:114-115 with is_first.
+__device__ __forceinline__ float first_preact(int in_dim, float t0, float t1, float w0, float w1, float b) {
+  return (in_dim == 1) ? __builtin_fmaf(t0, w0, b) : __builtin_fmaf(t1, w1, t0 * w0) + b;
+}
+
+// sin / cos of a (radians) for |a| < 2^17 via v_sin_f32 / v_cos_f32, which take revolutions:
+//   r = fma(a, inv2pi_hi, -n) + a * inv2pi_lo,  n = rint(a * inv2pi_hi)
+// fma forms a*inv2pi_hi - n with one rounding (|r| <= 1/2: error <= 2^-25 rev), the low part
+// adds < 2e-4 rev with 2^-24 relative error, so r is within ~4e-8 rev (2.5e-7 rad) of a/(2pi)
+// mod 1.  (OCML's sincosf with its large-argument reduction was 3x slower.)
+__device__ __forceinline__ float rev_reduce(float a) {
+  constexpr float kHi = 0x1.45f306p-3f;  // fp32(1/(2*pi))             0x3E22F983
+  constexpr float kLo = 0x1.b93910p-28f; // fp32(1/(2*pi) - kHi) = 6.42e-9  0x31DC9C88
+  const float n = __builtin_rintf(a * kHi);
+  return __builtin_fmaf(a, kLo, __builtin_fmaf(a, kHi, -n));
+}
+__device__ __forceinline__ void sincos_rev(float a, float* s, float* c) {
+  const float r = rev_reduce(a);
+  *s = __builtin_amdgcn_sinf(r);
+  *c = __builtin_amdgcn_cosf(r);
+}
+
 __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const LDS_AS char*)(p);
 }

@@ -119,7 +119,7 @@ def main():
     stagger = {k: 0 for k in cases}
     for v in [int(x) for x in args.staggers.split(",") if x]:
         for k, c in list(cases.items()):
-            if v and k.endswith("p1") and not k.startswith("dw") and stagger[k] == 0:
+            if v and (k.endswith("p1") or k.endswith("p4")) and not k.startswith("dw") and stagger[k] == 0:
                 cases[f"{k}_s{v}"] = c
                 stagger[f"{k}_s{v}"] = v
     diag = {k: 0 for k in cases}
