@@ -279,7 +279,8 @@ enum siren_prof_kind {
  * values so every block walks several tiles);
  * SIREN_OPT_NT_DIAG = measurement-only NT ablations (results are WRONG while set): bit 0 reads
  *   the X operand from the first 4 row bands only (L2-resident operand), bit 1 drops the
- *   epilogue's global stores (values kept live);
+ *   epilogue's global stores (values kept live), bit 2 replaces the forward's sin / cos by
+ *   the identity;
  * SIREN_OPT_NT_STAGGER = persistent NT start stagger: block b idles (b % 16) * value units of
  * ~1.7k cycles before its first tile, so that the blocks' epilogue store bursts do not
  * coincide (0 = none; 0..64). */

@@ -219,6 +219,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // and drops the store
   auto st16 = [&](h16* dst, uint4 v) {
     if (p.diag & 2) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+    else if (p.diag & 8) {
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (u32x4*)dst);
+    }
     else *(uint4*)dst = v;
   };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
@@ -298,8 +302,13 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                 // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
                 // hardware sin/cos inside their reduced domain for any magnitude.
                 const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
-                s[r] = __builtin_amdgcn_sinf(x);
-                c[r] = __builtin_amdgcn_cosf(x);
+                if (p.diag & 4) {  // measurement only: no transcendentals
+                  s[r] = x;
+                  c[r] = x;
+                } else {
+                  s[r] = __builtin_amdgcn_sinf(x);
+                  c[r] = __builtin_amdgcn_cosf(x);
+                }
               }
             } else if constexpr (MODE == NT_FWD_SNAKE) {
               const float4 a4 = *(const float4*)(a_lds + nq + i * 16);
