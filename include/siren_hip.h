@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 3
+#define SIREN_ABI_VERSION 4
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 
@@ -70,6 +70,12 @@ typedef struct siren_net {
   const float* b_head;                      /* [1]                          */
   int32_t act[SIREN_MAX_INNER];             /* siren_act of inner layer i   */
   const float* a[SIREN_MAX_INNER];          /* [H] Snake a (SNAKE layers)   */
+  /* first_linear=True (models.py:330-333): net.0 is Linear(in, H) + Snake(a0) instead of the
+   * first SineLayer (omega0 unused); last_linear=False (models.py:383-385): the last layer is
+   * SineLayer(H, 1, head_omega) -- out = sin(head_omega (Y w^T + b)); 0 = the final Linear */
+  int32_t first_snake, pad1;
+  const float* a0;                          /* [H] (first_snake)            */
+  float head_omega, pad2;
 } siren_net;
 
 /* gradient destinations (fp32, accumulated into: zero them, or set zero_grads) */
@@ -80,6 +86,7 @@ typedef struct siren_grads {
   float* sse;                               /* [1] sum of squared errors of valid rows */
   float* flat; int64_t flat_len;            /* if flat != NULL and zero_grads: memset   */
   float* a[SIREN_MAX_INNER];                /* [H] Snake a gradients (SNAKE layers)     */
+  float* a0;                                /* [H] first-layer Snake a (first_snake)    */
 } siren_grads;
 
 /* per-micro-batch activations and workspace; sizes from siren_workspace_floats() */
@@ -102,12 +109,13 @@ typedef struct siren_batch {
   float* gsum_part;      /* [rows/256]                                          */
   float* gmax_part;      /* [rows/256]  max |g| per block (train / backward)    */
   float* gscale;         /* [2]  {S, 1/S} of this micro-batch's backward        */
-  float* col_part;       /* [rows/128][1+in][H]                                 */
+  float* col_part;       /* [rows/128][max(2, 2+in)][H]                         */
   float* col_part2;      /* [rows/128][H]                                       */
   float* red_tmp;        /* [64][H]                                             */
   float* slab;           /* [splits][H][H]                                      */
   uint16_t* E[SIREN_MAX_INNER + 1];  /* E[i+1] fp16 [rows][H]: dY/da of Snake inner layer
-                                        i (NULL for other layers)                      */
+                                        i; E[0]: of a Linear + Snake first layer (NULL
+                                        for other layers)                              */
   /* optional gradient-ready events (hipEvent_t, NULL = none), recorded on `stream` as soon
    * as a bucket's gradients are final in this call -- set them on the LAST micro-batch so a
    * data-parallel caller can all-reduce each bucket on a communication stream while the rest

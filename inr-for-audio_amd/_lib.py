@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_INNER = 16
 ROW_TILE = 128
 ACT_SINE, ACT_SNAKE, ACT_TANH = 0, 1, 2  # siren_act
@@ -44,6 +44,7 @@ class SirenNet(ctypes.Structure):
         ("b", _p * MAX_INNER), ("Wh", _p * MAX_INNER), ("WTh", _p * MAX_INNER),
         ("w_head", _p), ("b_head", _p),
         ("act", _i32 * MAX_INNER), ("a", _p * MAX_INNER),
+        ("first_snake", _i32), ("pad1", _i32), ("a0", _p), ("head_omega", ctypes.c_float), ("pad2", ctypes.c_float),
     ]
 
 
@@ -53,7 +54,7 @@ class SirenGrads(ctypes.Structure):
         ("W", _p * MAX_INNER), ("b", _p * MAX_INNER),
         ("w_head", _p), ("b_head", _p), ("sse", _p),
         ("flat", _p), ("flat_len", _i64),
-        ("a", _p * MAX_INNER),
+        ("a", _p * MAX_INNER), ("a0", _p),
     ]
 
 

@@ -62,6 +62,8 @@ int check_net(const siren_net* n) {
     if (n->act[i] < SIREN_ACT_SINE || n->act[i] > SIREN_ACT_TANH) return SIREN_ERR_CONFIG;
     if (n->act[i] == SIREN_ACT_SNAKE && !n->a[i]) return SIREN_ERR_NULL;
   }
+  if (n->first_snake && !n->a0) return SIREN_ERR_NULL;
+  if (!(n->head_omega >= 0.f)) return SIREN_ERR_CONFIG;
   return SIREN_OK;
 }
 
@@ -83,6 +85,7 @@ int check_batch(const siren_net* n, const siren_batch* b, bool train) {
     if (!b->Y[i] || !b->C[i]) return SIREN_ERR_NULL;
   for (int i = 0; i < n->n_inner; ++i)
     if (n->act[i] == SIREN_ACT_SNAKE && !b->E[i + 1]) return SIREN_ERR_NULL;
+  if (n->first_snake && !b->E[0]) return SIREN_ERR_NULL;
   if (train) {
     if (!b->target || !b->dZ[0] || !b->dZ[1] || !b->col_part || !b->col_part2 || !b->red_tmp ||
         !b->slab || !b->gmax_part || !b->gscale)
@@ -101,7 +104,8 @@ inline hipError_t mark_ready(const siren_batch* b, int k, hipStream_t s) {
 hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s) {
   const int R = b->rows, H = n->hidden, L = n->n_inner;
   SIREN_PROF(SIREN_PROF_FIRST_FWD, s, first_fwd(b->coords, n->in_dim, n->W0, n->b0, n->omega0, R, H, B(b->Y[0]),
-                                                B(b->C[0]), s));
+                                                B(b->C[0]), s, n->first_snake ? n->a0 : nullptr,
+                                                n->first_snake ? B(b->E[0]) : nullptr));
   for (int i = 0; i < L; ++i) {
     NtParams p = {};
     p.X = B(b->Y[i]);
@@ -167,7 +171,8 @@ int siren_forward(const siren_net* net, siren_batch* batch, void* stream) {
   // out = sum of head partials + bias (g/sse unused at inference: n_valid = 0 path)
   SIREN_TRY(head_loss(batch->head_part, net->hidden / nt_choose_tile(batch->rows, net->hidden),
                       batch->rows, net->b_head, batch->out,
-                      0, 0.f, batch->out, batch->g, batch->sse_part, batch->gsum_part, nullptr, s));
+                      0, 0.f, batch->out, batch->g, batch->sse_part, batch->gsum_part, nullptr, s,
+                      net->head_omega));
   return SIREN_OK;
 }
 
@@ -177,6 +182,7 @@ static int check_grads(const siren_net* net, const siren_grads* gr) {
     if (!gr->W[i] || !gr->b[i]) return SIREN_ERR_NULL;
     if (net->act[i] == SIREN_ACT_SNAKE && !gr->a[i]) return SIREN_ERR_NULL;
   }
+  if (net->first_snake && !gr->a0) return SIREN_ERR_NULL;
   return SIREN_OK;
 }
 
@@ -233,12 +239,17 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
                                                     b->red_tmp, s));
       cur ^= 1;
     } else {
-      p.omega = net->omega0;
+      const bool fs = net->first_snake != 0;
+      p.omega = fs ? 1.0f : net->omega0;
       p.Cprev = B(b->C[0]);
+      p.Eprev = B(b->E[0]);
       p.t = b->coords;
       p.in_dim = in;
-      SIREN_PROF(SIREN_PROF_BWD_DX0, s, gemm_nt(NT_DX0, false, p, s));
-      const int64_t rs = (int64_t)(1 + in) * H;
+      SIREN_PROF(SIREN_PROF_BWD_DX0, s, gemm_nt(fs ? NT_DX0_SNAKE : NT_DX0, false, p, s));
+      const int64_t rs = (int64_t)(fs ? 2 + in : 1 + in) * H;
+      if (fs)
+        SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + (int64_t)(1 + in) * H, rs, prow, H, gr->a0, 1, 1,
+                                                    b->red_tmp, s));
       SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, rs, prow, H, gr->b0, 1, 1, b->red_tmp, s));
       for (int j = 0; j < in; ++j)
         SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + (int64_t)(1 + j) * H, rs, prow, H,
@@ -265,7 +276,7 @@ int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b
   const float gfac = (float)(2.0 / b->n_total);  // MSELoss mean backward: 2/N
   SIREN_PROF(SIREN_PROF_HEAD, s, head_loss(b->head_part, H / nt_choose_tile(R, H), R, net->b_head,
                                            b->target, b->n_valid, gfac, b->out, b->g, b->sse_part,
-                                           b->gsum_part, b->gmax_part, s));
+                                           b->gsum_part, b->gmax_part, s, net->head_omega));
   const int nsum = (R + 255) / 256;
   SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->sse_part, nsum, gr->sse, 1, s));
   SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->gsum_part, nsum, gr->b_head, 1, s));
@@ -280,6 +291,10 @@ int siren_backward(const siren_net* net, const siren_grads* gr, siren_batch* b, 
   if ((st = check_grads(net, gr))) return st;
   hipStream_t s = S(stream);
   if (b->zero_grads && gr->flat) SIREN_TRY(hipMemsetAsync(gr->flat, 0, gr->flat_len * sizeof(float), s));
+  // last_linear=False: chain dLoss/dout through the final sin (head_part is the forward's)
+  if (net->head_omega > 0.f)
+    SIREN_TRY(head_sine_chain(b->head_part, net->hidden / nt_choose_tile(b->rows, net->hidden), b->rows,
+                              net->b_head, net->head_omega, b->g, s));
   // bias of the head: sum of g; max |g| partials for the backward storage scale
   SIREN_TRY(sum_to(b->g, b->rows, gr->b_head, 1, s));
   SIREN_TRY(gmax_partials(b->g, b->rows, b->gmax_part, s));

@@ -52,27 +52,41 @@ hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, 
 // recomputes the same cosine.)
 // Row-wise: each thread owns 8 columns (W0 / b0 in registers) and walks rows; a row is H/8
 // threads, a 256-thread block covers 256/(H/8) rows per pass; Y0 / C0 go out as 16-B pieces.
-template <bool STORE_C>
+// SNAKE (first_linear=True, models.py:330-333): Linear(in, H) + Snake(a0) --
+// Y0 = z + sin^2(a z)/a, C0 = 1 + sin(2az) (dY/dz), E0 = (z sin(2az) - sin^2(az)/a)/a (dY/da)
+template <bool STORE_C, bool SNAKE>
 __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const float* __restrict__ W0,
                                  const float* __restrict__ b0, float omega0, int R, int H,
-                                 h16* __restrict__ Y0, h16* __restrict__ C0) {
+                                 h16* __restrict__ Y0, h16* __restrict__ C0, const float* __restrict__ a0,
+                                 h16* __restrict__ E0) {
   const int tpr = H >> 3;
   const int rpb = blockDim.x / tpr;
   const int lt = threadIdx.x % tpr, lr = threadIdx.x / tpr;
   const int n = lt * 8;
-  float w0[8], w1[8], bb[8];
+  float w0[8], w1[8], bb[8], av[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     w0[r] = W0[(n + r) * in_dim];
     w1[r] = (in_dim > 1) ? W0[(n + r) * in_dim + 1] : 0.f;
     bb[r] = b0[n + r];
+    av[r] = SNAKE ? a0[n + r] : 0.f;
   }
   for (int64_t m = (int64_t)blockIdx.x * rpb + lr; m < R; m += (int64_t)gridDim.x * rpb) {
     const float t0 = t[m * in_dim];
     const float t1 = (in_dim > 1) ? t[m * in_dim + 1] : 0.f;
-    float y[8], c[8];
+    float y[8], c[8], ev[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
+      if constexpr (SNAKE) {
+        const float z = first_preact(in_dim, t0, t1, w0[r], w1[r], bb[r]);
+        float sn, cn;
+        sincos_rev(z * av[r], &sn, &cn);
+        const float ia = 1.0f / av[r], s2 = sn * sn, sc2 = 2.0f * sn * cn;
+        y[r] = z + s2 * ia;
+        c[r] = 1.0f + sc2;
+        ev[r] = (z * sc2 - s2 * ia) * ia;
+        continue;
+      }
       sincos_rev(omega0 * first_preact(in_dim, t0, t1, w0[r], w1[r], bb[r]), &y[r], &c[r]);
     }
     h16x8 yv, cv;
@@ -83,20 +97,31 @@ __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const 
     }
     *(h16x8*)(Y0 + m * H + n) = yv;
     if constexpr (STORE_C) *(h16x8*)(C0 + m * H + n) = cv;
+    if constexpr (SNAKE) {
+      h16x8 evv;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) evv[r] = (h16)ev[r];
+      *(h16x8*)(E0 + m * H + n) = evv;
+    }
   }
 }
 
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
-                     int R, int H, h16* Y0, h16* C0, hipStream_t s) {
+                     int R, int H, h16* Y0, h16* C0, hipStream_t s, const float* a0, h16* E0) {
   if (H % 8 || H > 2048 || 256 % (H / 8) || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
+  if ((a0 != nullptr) != (E0 != nullptr) || (a0 && !C0)) return hipErrorInvalidValue;
   const int rpb = 256 / (H / 8);
-  // C0 == NULL: the fused train step recomputes cos in the layer-0 dX epilogue (NT_DX0R)
-  if (C0)
-    hipLaunchKernelGGL(first_fwd_kernel<true>, dim3(grid_for(R, rpb, 4096)), dim3(256), 0, s, t, in_dim, W0, b0,
-                       omega0, R, H, Y0, C0);
+  const dim3 grid(grid_for(R, rpb, 4096));
+  // C0 == NULL: Y0 only (the cos is not needed); a0 != NULL: Linear + Snake first layer
+  if (a0)
+    hipLaunchKernelGGL((first_fwd_kernel<true, true>), grid, dim3(256), 0, s, t, in_dim, W0, b0, omega0, R, H, Y0,
+                       C0, a0, E0);
+  else if (C0)
+    hipLaunchKernelGGL((first_fwd_kernel<true, false>), grid, dim3(256), 0, s, t, in_dim, W0, b0, omega0, R, H, Y0,
+                       C0, a0, E0);
   else
-    hipLaunchKernelGGL(first_fwd_kernel<false>, dim3(grid_for(R, rpb, 4096)), dim3(256), 0, s, t, in_dim, W0, b0,
-                       omega0, R, H, Y0, C0);
+    hipLaunchKernelGGL((first_fwd_kernel<false, false>), grid, dim3(256), 0, s, t, in_dim, W0, b0, omega0, R, H, Y0,
+                       C0, a0, E0);
   return hipGetLastError();
 }
 
@@ -109,7 +134,8 @@ __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts
                                  const float* __restrict__ b_head, const float* __restrict__ y,
                                  int n_valid, float gfac, float* __restrict__ out,
                                  float* __restrict__ g, float* __restrict__ sse_part,
-                                 float* __restrict__ gsum_part, float* __restrict__ gmax_part) {
+                                 float* __restrict__ gsum_part, float* __restrict__ gmax_part,
+                                 float head_omega) {
   __shared__ float scratch[4];
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   float e2 = 0.f, gv = 0.f;
@@ -117,11 +143,16 @@ __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts
     float o = 0.f;
     for (int j = 0; j < nparts; ++j) o += head_part[(size_t)j * R + m];
     o += b_head[0];
-    out[m] = o;
+    // last_linear=False: the last layer is SineLayer(H, 1, omega) -- out = sin(omega * o) and
+    // g is the gradient at the linear output o: 2(out - y)/N * cos(omega o) * omega
+    const float a = head_omega * o;
+    const float ov = head_omega > 0.f ? sinf(a) : o;
+    out[m] = ov;
     if (m < n_valid) {
-      const float err = o - y[m];
+      const float err = ov - y[m];
       e2 = err * err;
       gv = err * gfac;
+      if (head_omega > 0.f) gv = (gv * cosf(a)) * head_omega;
     }
     g[m] = gv;
   }
@@ -137,9 +168,28 @@ __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts
 
 hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_head, const float* y,
                      int n_valid, float gfac, float* out, float* g, float* sse_part,
-                     float* gsum_part, float* gmax_part, hipStream_t s) {
+                     float* gsum_part, float* gmax_part, hipStream_t s, float head_omega) {
   hipLaunchKernelGGL(head_loss_kernel, dim3((R + 255) / 256), dim3(256), 0, s, head_part, nparts, R,
-                     b_head, y, n_valid, gfac, out, g, sse_part, gsum_part, gmax_part);
+                     b_head, y, n_valid, gfac, out, g, sse_part, gsum_part, gmax_part, head_omega);
+  return hipGetLastError();
+}
+
+// last_linear=False in siren_backward: dLoss/dout -> dLoss/do at the final SineLayer's linear
+// output o = sum head_part + b (kept from the forward): g *= cos(omega o) * omega
+__global__ void head_sine_chain_kernel(const float* __restrict__ head_part, int nparts, int R,
+                                       const float* __restrict__ b_head, float omega, float* __restrict__ g) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= R) return;
+  float o = 0.f;
+  for (int j = 0; j < nparts; ++j) o += head_part[(size_t)j * R + m];
+  o += b_head[0];
+  g[m] = (g[m] * cosf(omega * o)) * omega;
+}
+
+hipError_t head_sine_chain(const float* head_part, int nparts, int R, const float* b_head, float omega, float* g,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(head_sine_chain_kernel, dim3((R + 255) / 256), dim3(256), 0, s, head_part, nparts, R, b_head,
+                     omega, g);
   return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 //            E = (z sin(2az) - sin^2(az)/a)/a (dY/da)                      -- models.py:235-241
 //   NT_FWD_TANH  : z = acc + b;  Y = tanh z, C = 1 - Y^2                    -- models.py:366-372
 //   NT_DX_SNAKE  : dz = acc * D (Cprev) + column partials of dz (db) and acc * E (da)
+//   NT_DX0_SNAKE : same into a Linear + Snake first layer (Cprev = D0, omega 1) + da0 partials
 //   NT_DX0 : same, into the fp32 first layer (Cprev = its cos from first_fwd): only the
 //            column partial sums of dz and dz*t_j (db0, dW0) are written; dZ0 never
 //            reaches HBM.
@@ -66,7 +67,7 @@ struct NtCfg {
   static constexpr int RING = S * STAGE;
   // epilogue scratch behind the ring: HEAD row partials [WN][BM] or column sums [3][WM][BN],
   // then (NT_FWD) the whole bias and head weight vectors, staged once per block
-  static constexpr int RED = 4 * (WN * BM > 3 * WM * BN ? WN * BM : 3 * WM * BN);
+  static constexpr int RED = 4 * (WN * BM > 4 * WM * BN ? WN * BM : 4 * WM * BN);
   static constexpr int MAXN = 1024;
   static constexpr int VEC = 4 * MAXN;  // one per-column fp32 vector
   static constexpr int XINSTR = XBYTES / 1024 / NWAVES;  // LDS-DMA instructions per wave per stage
@@ -102,6 +103,8 @@ struct NtLds {
   static constexpr int PF = A + (MODE == NT_FWD_SNAKE ? Cfg::VEC : 0);
   static constexpr int SIZE = PF + (Cfg::PF ? 256 : 0);
 };
+
+constexpr bool nt_is_dx0(int m) { return m == NT_DX0 || m == NT_DX0_SNAKE; }
 
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp)
           cp_in[j][pp] = *(const uint4*)(p.Cprev + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
-      if constexpr (MODE == NT_DX0) {
+      if constexpr (nt_is_dx0(MODE)) {
 #pragma unroll
         for (int j = 0; j < SM; ++j) {
           const size_t m = mrow0 + j * 16;
@@ -365,11 +368,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     } else {
       // column sums over this tile's BM rows (db / dW0 partials): per lane over its SM row
       // tiles, over the 16 row-lanes by DPP, then over the WM row waves through LDS.
-      const int in_dim = (MODE == NT_DX0) ? p.in_dim : 0;
-      const int nred = (MODE == NT_DX_SNAKE) ? 2 : 1 + in_dim;
-      float cs[3][SN][4];
+      const int in_dim = nt_is_dx0(MODE) ? p.in_dim : 0;
+      const int nred = (MODE == NT_DX_SNAKE) ? 2 : (MODE == NT_DX0_SNAKE ? 2 + in_dim : 1 + in_dim);
+      // slots: 0 db; 1..in dW0 (NT_DX0*); 1 da (NT_DX_SNAKE); 3 da0 (NT_DX0_SNAKE, written as 1+in)
+      float cs[4][SN][4];
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int i = 0; i < SN; ++i)
 #pragma unroll
@@ -381,7 +385,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         const int m = mrow0 + j * 16;
         const size_t rowoff = (size_t)m * N;
         float t0 = 0.f, t1 = 0.f;
-        if constexpr (MODE == NT_DX0) {
+        if constexpr (nt_is_dx0(MODE)) {
           t0 = t_in[j][0];
           t1 = t_in[j][1];
         }
@@ -392,7 +396,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                                         : *(const uint4*)(p.Cprev + rowoff + npc + pp * 32);
           unswap16_pair(cpv, cpu[0], cpu[1]);
           uint2 epu[2];
-          if constexpr (MODE == NT_DX_SNAKE)
+          if constexpr (MODE == NT_DX_SNAKE || MODE == NT_DX0_SNAKE)
             unswap16_pair(*(const uint4*)(p.Eprev + rowoff + npc + pp * 32), epu[0], epu[1]);
           uint2 dzp[2];
 #pragma unroll
@@ -404,11 +408,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             for (int r = 0; r < 4; ++r) {
               dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
               cs[0][i][r] += dz[r];
-              if constexpr (MODE == NT_DX0) {
+              if constexpr (nt_is_dx0(MODE)) {
                 cs[1][i][r] += dz[r] * t0;
                 cs[2][i][r] += dz[r] * t1;
               }
               if constexpr (MODE == NT_DX_SNAKE) cs[1][i][r] += acc[i][j][r] * (float)as_h4(epu[h])[r];
+              if constexpr (MODE == NT_DX0_SNAKE) cs[3][i][r] += acc[i][j][r] * (float)as_h4(epu[h])[r];
             }
             dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
           }
@@ -419,13 +424,15 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       // partial layout: NT_DX [tm][N]; NT_DX0 [tm][1+in][N] with q=0 -> db0, q=1+j -> dW0[:, j];
       // NT_DX_SNAKE [tm][2][N] with q=0 -> db, q=1 -> da
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < 4; ++q) {
         if (q >= nred) break;
+        // NT_DX0_SNAKE: da0 (slot 3) goes out as partial row 1 + in
+        const bool da0 = (MODE == NT_DX0_SNAKE) && q == nred - 1;
 #pragma unroll
         for (int i = 0; i < SN; ++i) {
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[q][i][r]);
+          for (int r = 0; r < 4; ++r) v[r] = row16_sum(da0 ? cs[3][i][r] : cs[q][i][r]);
           if ((lane & 15) == 0)
             *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + i * 16 + 4 * (lane >> 4)) =
                 float4{v[0], v[1], v[2], v[3]};
@@ -575,6 +582,12 @@ static hipError_t dispatch_mode(int mode, bool head, const NtParams& p, hipStrea
   return hipErrorInvalidValue;
 }
 
+// first_linear=True: dX into the Linear + Snake first layer (default persistent K-loop / 128 tile)
+template <class Cfg>
+static hipError_t dispatch_dx0_snake(const NtParams& p, hipStream_t s, bool persistent) {
+  return launch_nt<Cfg, NT_DX0_SNAKE, false>(p, s, persistent);
+}
+
 // Snake / Tanh layers: the default persistent K-loop (or the 128x128 tile)
 template <class Cfg>
 static hipError_t dispatch_act(int mode, bool head, const NtParams& p, hipStream_t s, bool persistent) {
@@ -608,7 +621,16 @@ int nt_choose_tile(int M, int N) {
 
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (p.M % NtSmall::BM || p.N % NtSmall::BN || p.K % NtSmall::BK || p.M <= 0 || p.N > NtSmall::MAXN) return hipErrorInvalidValue;
-  if (mode == NT_DX0 && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
+  if (nt_is_dx0(mode) && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
+  if (mode == NT_DX0_SNAKE) {
+    if (!p.Eprev) return hipErrorInvalidValue;
+    if (p.tile == 256) {
+      if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
+      return dispatch_dx0_snake<NtLarge>(p, s, true);
+    }
+    if (p.tile != 128) return hipErrorInvalidValue;
+    return dispatch_dx0_snake<NtSmall>(p, s, false);
+  }
   if (mode >= NT_FWD_SNAKE) {
     if ((mode == NT_FWD_SNAKE && (!p.act_a || !p.E)) || (mode == NT_DX_SNAKE && !p.Eprev))
       return hipErrorInvalidValue;

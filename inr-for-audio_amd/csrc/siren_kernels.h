@@ -10,7 +10,10 @@ typedef _Float16 h16;  // activation / weight-shadow / gradient storage (fp16, s
 
 // NT_FWD_SNAKE / NT_FWD_TANH: Linear + Snake / Tanh forward epilogues; NT_DX_SNAKE: dX into
 // a Snake layer (derivative D and d/da E of the layer below), SURVEY §8 f3
-enum NtMode { NT_FWD = 0, NT_DX = 1, NT_DX0 = 2, NT_FWD_SNAKE = 3, NT_FWD_TANH = 4, NT_DX_SNAKE = 5 };
+// NT_DX0_SNAKE: dX into a Linear + Snake first layer (first_linear=True): dz = acc * D0, partials
+// of db0, dW0 (x t_j) and da0 = sum acc * E0
+enum NtMode { NT_FWD = 0, NT_DX = 1, NT_DX0 = 2, NT_FWD_SNAKE = 3, NT_FWD_TANH = 4, NT_DX_SNAKE = 5,
+              NT_DX0_SNAKE = 6 };
 constexpr bool nt_is_fwd(int m) { return m == NT_FWD || m == NT_FWD_SNAKE || m == NT_FWD_TANH; }
 
 struct NtParams {
@@ -31,7 +34,8 @@ struct NtParams {
   const h16* Cprev;    // [M][N]  cos of the layer below (NT_DX); D of a Snake / 1-y^2 of a Tanh
   const h16* Eprev;    // [M][N]  NT_DX_SNAKE: E of the Snake layer below
   h16* dZ;             // [M][N]  (NT_DX)
-  float* colsum_part;   // NT_DX: [M/128][N];  NT_DX0: [M/128][1+in][N];  NT_DX_SNAKE: [M/128][2][N]
+  float* colsum_part;   // NT_DX: [M/128][N];  NT_DX0: [M/128][1+in][N];  NT_DX_SNAKE: [M/128][2][N];
+                        // NT_DX0_SNAKE: [M/128][2+in][N] (db0, dW0[:, j], da0)
   // NT_DX0 (Cprev = cos of the first layer)
   const float* t;       // [M][in]
   int in_dim;
@@ -71,12 +75,16 @@ hipError_t dw_reduce(const float* slab, int splits, int Hin, int Hout, int tile,
 
 // elementwise / reduction kernels (elementwise.hip)
 hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, hipStream_t s);
+// a0 / E0 non-null: Linear + Snake first layer (first_linear=True); C0 null: Y0 only
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
-                     int R, int H, h16* Y0, h16* C0, hipStream_t s);
+                     int R, int H, h16* Y0, h16* C0, hipStream_t s, const float* a0 = nullptr,
+                     h16* E0 = nullptr);
 hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_head, const float* y,
                      int n_valid, float gfac, float* out, float* g, float* sse_part,
-                     float* gsum_part, float* gmax_part, hipStream_t s);
+                     float* gsum_part, float* gmax_part, hipStream_t s, float head_omega = 0.f);
 hipError_t gmax_partials(const float* g, int R, float* gmax_part, hipStream_t s);
+hipError_t head_sine_chain(const float* head_part, int nparts, int R, const float* b_head, float omega, float* g,
+                           hipStream_t s);
 // gscale[0] = S (dZ storage scale), gscale[1] = 1/S; from (R+255)/256 max|g| partials
 hipError_t grad_scale(const float* gmax_part, int nparts, const float* w_head, int H, float omega,
                       float* gscale, hipStream_t s);

@@ -45,6 +45,8 @@ class NetSpec:
     omega0: float
     omega: float
     acts: tuple = ()   # siren_act per inner layer (empty: all sine)
+    first_snake: bool = False   # first_linear=True: net.0 is Linear + Snake
+    head_omega: float = 0.0     # last_linear=False: final SineLayer(H, 1, head_omega)
 
     def act(self, i: int) -> int:
         return self.acts[i] if self.acts else _lib.ACT_SINE
@@ -94,7 +96,8 @@ class Workspace:
         self.Y = [e(R, H, dtype=h) for _ in range(L + 1)]
         self.C = [e(R, H, dtype=h) for _ in range(L + 1)]
         # dY/da of Snake layers (E[i+1] for inner layer i)
-        self.E = [None] + [e(R, H, dtype=h) if spec.act(i) == _lib.ACT_SNAKE else None for i in range(L)]
+        self.E = [e(R, H, dtype=h) if spec.first_snake else None] + \
+            [e(R, H, dtype=h) if spec.act(i) == _lib.ACT_SNAKE else None for i in range(L)]
         self.out = e(R)
         self.g = torch.zeros(R, dtype=f32, device=device)
         self.head_part = e(H // 128, R)
@@ -107,7 +110,7 @@ class Workspace:
         if train:
             self.splits = int(splits or lib.siren_default_splits(R, H))
             self.dZ = [e(R, H, dtype=h) for _ in range(2)]
-            self.col_part = e(R // 128, max(1 + spec.in_dim, 2), H)
+            self.col_part = e(R // 128, max(2 + spec.in_dim, 2), H)
             self.col_part2 = e(R // 128, H)
             self.red_tmp = e(64, H)
             self.slab = e(int(lib.siren_slab_floats(H, self.splits)))
@@ -137,7 +140,7 @@ class Workspace:
         return b
 
 
-def make_net(spec: NetSpec, W0, b0, bs, Whs, WThs, w_head, b_head, snake_a=None) -> SirenNet:
+def make_net(spec: NetSpec, W0, b0, bs, Whs, WThs, w_head, b_head, snake_a=None, a0=None) -> SirenNet:
     n = SirenNet()
     n.in_dim, n.hidden, n.n_inner = spec.in_dim, spec.hidden, spec.n_inner
     n.omega0, n.omega = spec.omega0, spec.omega
@@ -148,6 +151,9 @@ def make_net(spec: NetSpec, W0, b0, bs, Whs, WThs, w_head, b_head, snake_a=None)
         if snake_a is not None and snake_a[i] is not None:
             n.a[i] = ptr(snake_a[i])
     n.w_head, n.b_head = ptr(w_head), ptr(b_head)
+    n.first_snake = int(spec.first_snake)
+    n.a0 = ptr(a0)
+    n.head_omega = float(spec.head_omega)
     return n
 
 
@@ -162,6 +168,8 @@ def make_grads(spec: NetSpec, layout: ParamLayout, gflat: torch.Tensor, ix: dict
         if ix["a"][i] is not None:
             g.a[i] = ptr(v(ix["a"][i]))
     g.w_head, g.b_head = ptr(v(ix["wh"])), ptr(v(ix["bh"]))
+    if ix.get("a0") is not None:
+        g.a0 = ptr(v(ix["a0"]))
     g.sse = gflat.data_ptr() + 4 * layout.sse_offset
     g.flat, g.flat_len = ptr(gflat), layout.flat_len
     return g
@@ -230,7 +238,8 @@ class SirenEngine:
         self.Wh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
         self.WTh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
         self.net = make_net(spec, pv(ix["W0"]), pv(ix["b0"]), [pv(k) for k in ix["b"]], self.Wh, self.WTh,
-                            pv(ix["wh"]), pv(ix["bh"]), [None if k is None else pv(k) for k in ix["a"]])
+                            pv(ix["wh"]), pv(ix["bh"]), [None if k is None else pv(k) for k in ix["a"]],
+                            None if ix["a0"] is None else pv(ix["a0"]))
         self.grad_struct = make_grads(spec, lay, self.grads, ix)
         self._Wp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.W])
         self._Whp = (ctypes.c_void_p * L)(*[ptr(w) for w in self.Wh])
@@ -288,7 +297,7 @@ class SirenEngine:
         for i in range(L - 1, -1, -1):
             ids = [ix["W"][i], ix["b"][i]] + ([ix["a"][i]] if ix["a"][i] is not None else [])
             order.append((i,) + span(ids))
-        order.append((L,) + span([ix["W0"], ix["b0"]]))
+        order.append((L,) + span([ix["W0"], ix["b0"]] + ([ix["a0"]] if ix["a0"] is not None else [])))
         self._events = []
         for _ in range(L + 2):
             ev = torch.cuda.Event()

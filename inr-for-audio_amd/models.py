@@ -76,9 +76,10 @@ class Snake(nn.Module):
 
 class SirenWithSnakeTanh(nn.Module):
     """MLP with sine / Snake / Tanh activations -- models.py:306-394.  The HIP path covers
-    a first SineLayer, then num_sine SineLayers, num_snake Linear+Snake and num_tanh
-    Linear+Tanh hidden layers, and the final Linear (first_linear=False, last_linear=True,
-    the reference train()'s defaults)."""
+    every configuration of the reference's constructor: a first SineLayer or (first_linear)
+    a first Linear+Snake, then num_sine SineLayers, num_snake Linear+Snake and num_tanh
+    Linear+Tanh hidden layers, then the final Linear or (last_linear=False) a final
+    SineLayer(H, 1)."""
 
     def __init__(self, in_features, out_features, hidden_features, num_sine, num_snake, num_tanh,
                  first_linear=False, last_linear=True, first_omega_0=30, hidden_omega_0=30.,
@@ -118,10 +119,6 @@ class SirenWithSnakeTanh(nn.Module):
     def hip_spec(self):
         """NetSpec of the fused path; raises for configurations it does not cover."""
         from .engine import NetSpec
-        if self.first_linear or not self.last_linear:
-            raise NotImplementedError(
-                "HIP path: first_linear=False and last_linear=True (a first Linear+Snake or a "
-                "final SineLayer has no fused kernel)")
         if self.out_features != 1:
             raise NotImplementedError("HIP path: out_features must be 1 (run.py:95,112)")
         n_inner = self.num_sine + self.num_snake + self.num_tanh
@@ -138,7 +135,8 @@ class SirenWithSnakeTanh(nn.Module):
         acts = (_lib.ACT_SINE,) * self.num_sine + (_lib.ACT_SNAKE,) * self.num_snake + \
             (_lib.ACT_TANH,) * self.num_tanh
         return NetSpec(self.in_features, H, n_inner, float(self.first_omega_0),
-                       float(self.hidden_omega_0), acts)
+                       float(self.hidden_omega_0), acts, bool(self.first_linear),
+                       0.0 if self.last_linear else float(self.hidden_omega_0))
 
     def param_index(self):
         """Positions in named_parameters() order (== state_dict order == Adam's state index)
@@ -147,9 +145,15 @@ class SirenWithSnakeTanh(nn.Module):
         net.{i}.{weight,bias} + net.{i+1}.a; Linear+Tanh: net.{i}.{weight,bias}."""
         names = [n for n, _ in self.named_parameters()]
         pos = {n: k for k, n in enumerate(names)}
-        idx = {"W0": pos["net.0.linear.weight"], "b0": pos["net.0.linear.bias"], "W": [], "b": [], "a": []}
+        if self.first_linear:  # net.0 Linear, net.1 Snake (models.py:330-333)
+            idx = {"W0": pos["net.0.weight"], "b0": pos["net.0.bias"], "a0": pos["net.1.a"], "W": [], "b": [],
+                   "a": []}
+            j = 2
+        else:
+            idx = {"W0": pos["net.0.linear.weight"], "b0": pos["net.0.linear.bias"], "a0": None, "W": [], "b": [],
+                   "a": []}
+            j = 1
         mods = list(self.net)
-        j = 1
         for _ in range(self.num_sine):
             idx["W"].append(pos[f"net.{j}.linear.weight"])
             idx["b"].append(pos[f"net.{j}.linear.bias"])
@@ -160,8 +164,11 @@ class SirenWithSnakeTanh(nn.Module):
             idx["b"].append(pos[f"net.{j}.bias"])
             idx["a"].append(pos[f"net.{j + 1}.a"] if kind == "snake" else None)
             j += 2
-        assert isinstance(mods[j], nn.Linear), "last layer must be the final Linear"
-        idx["wh"], idx["bh"] = pos[f"net.{j}.weight"], pos[f"net.{j}.bias"]
+        if self.last_linear:
+            assert isinstance(mods[j], nn.Linear), "last layer must be the final Linear"
+            idx["wh"], idx["bh"] = pos[f"net.{j}.weight"], pos[f"net.{j}.bias"]
+        else:  # final SineLayer(H, 1) (models.py:383-385)
+            idx["wh"], idx["bh"] = pos[f"net.{j}.linear.weight"], pos[f"net.{j}.linear.bias"]
         return idx
 
     def forward(self, coords):
@@ -196,7 +203,8 @@ class _SirenFunction(torch.autograd.Function):
         s = torch.cuda.current_stream(dev).cuda_stream
         cast_shadows(spec, W, Wh, WTh, s)
         net = make_net(spec, p[ix["W0"]], p[ix["b0"]], [p[k] for k in ix["b"]], Wh, WTh, p[ix["wh"]],
-                       p[ix["bh"]], [None if k is None else p[k] for k in ix["a"]])
+                       p[ix["bh"]], [None if k is None else p[k] for k in ix["a"]],
+                       None if ix["a0"] is None else p[ix["a0"]])
         ws = Workspace(spec, rows, dev, train=True)
         xc = torch.zeros(rows, spec.in_dim, dtype=torch.float32, device=dev)
         xc[:n] = coords.float()
@@ -229,6 +237,8 @@ class _SirenFunction(torch.autograd.Function):
             if ix["a"][i] is not None:
                 gs.a[i] = ptr(views[ix["a"][i]])
         gs.w_head, gs.b_head = ptr(views[ix["wh"]]), ptr(views[ix["bh"]])
+        if ix["a0"] is not None:
+            gs.a0 = ptr(views[ix["a0"]])
         gs.sse, gs.flat, gs.flat_len = flat.data_ptr() + 4 * off, ptr(flat), off + SEG_ALIGN
         b = ws.batch(xc, tgt, n, float(n))
         s = torch.cuda.current_stream(dev).cuda_stream

@@ -93,18 +93,30 @@ def waveform_target(data: np.ndarray, duration: int, sample_rate: int, decimatio
 
 
 # ------------------------------------------------------------------ model (models.py)
-def layer_keys(num_sine: int, num_snake: int = 0, num_tanh: int = 0):
-    """state_dict keys of SirenWithSnakeTanh (models.py:306-386, first_linear=False,
-    last_linear=True): per inner layer (kind, weight, bias, a-or-None), then the head's
-    (weight, bias).  SineLayer i: net.{i}.linear.*; Linear+Snake: net.{j}.* + net.{j+1}.a;
-    Linear+Tanh: net.{j}.* (net.{j+1} is the parameterless Tanh)."""
-    layers, j = [], 1
+def first_keys(first_linear: bool = False):
+    """(weight, bias, a-or-None) of net.0: SineLayer (net.0.linear.*) or, with first_linear,
+    Linear + Snake (net.0.*, net.1.a; models.py:330-333)."""
+    if first_linear:
+        return "net.0.weight", "net.0.bias", "net.1.a"
+    return "net.0.linear.weight", "net.0.linear.bias", None
+
+
+def layer_keys(num_sine: int, num_snake: int = 0, num_tanh: int = 0, first_linear: bool = False,
+               last_linear: bool = True):
+    """state_dict keys of SirenWithSnakeTanh (models.py:306-386): per inner layer (kind,
+    weight, bias, a-or-None), then the head's (weight, bias).  SineLayer i: net.{i}.linear.*;
+    Linear+Snake: net.{j}.* + net.{j+1}.a; Linear+Tanh: net.{j}.* (net.{j+1} is the
+    parameterless Tanh); the head is a Linear (net.{j}.*) or, without last_linear, a
+    SineLayer (net.{j}.linear.*)."""
+    layers, j = [], 2 if first_linear else 1
     for _ in range(num_sine):
         layers.append(("sine", f"net.{j}.linear.weight", f"net.{j}.linear.bias", None))
         j += 1
     for kind in ["snake"] * num_snake + ["tanh"] * num_tanh:
         layers.append((kind, f"net.{j}.weight", f"net.{j}.bias", f"net.{j + 1}.a" if kind == "snake" else None))
         j += 2
+    if not last_linear:
+        return layers, (f"net.{j}.linear.weight", f"net.{j}.linear.bias")
     return layers, (f"net.{j}.weight", f"net.{j}.bias")
 
 
@@ -113,7 +125,7 @@ class Params:
     b[i] [H], a[i] [H] (Snake layers, else None), wf [H] (= head weight[0]), bf scalar;
     kinds[i] in {'sine', 'snake', 'tanh'}."""
 
-    def __init__(self, W0, b0, W, b, wf, bf, kinds=None, a=None):
+    def __init__(self, W0, b0, W, b, wf, bf, kinds=None, a=None, a0=None, head_omega=0.0):
         self.W0, self.b0 = np.asarray(W0, F32), np.asarray(b0, F32)
         self.W = [np.asarray(w, F32) for w in W]
         self.b = [np.asarray(x, F32) for x in b]
@@ -121,22 +133,33 @@ class Params:
         self.bf = F32(np.asarray(bf).reshape(-1)[0])
         self.kinds = list(kinds) if kinds is not None else ["sine"] * len(self.W)
         self.a = [None if x is None else np.asarray(x, F32).reshape(-1) for x in (a or [None] * len(self.W))]
+        self.a0 = None if a0 is None else np.asarray(a0, F32).reshape(-1)   # first_linear Snake a
+        self.head_omega = float(head_omega)                                 # >0: final SineLayer
 
     def counts(self):
         return self.kinds.count("sine"), self.kinds.count("snake"), self.kinds.count("tanh")
 
+    def keys(self):
+        return layer_keys(*self.counts(), first_linear=self.a0 is not None, last_linear=self.head_omega == 0)
+
     @classmethod
-    def from_state_dict(cls, sd: dict, n_inner: int, num_snake: int = 0, num_tanh: int = 0):
+    def from_state_dict(cls, sd: dict, n_inner: int, num_snake: int = 0, num_tanh: int = 0,
+                        first_linear: bool = False, last_linear: bool = True, hidden_omega: float = 30.0):
         """n_inner = num_sine (the sine-only form) when num_snake = num_tanh = 0."""
         g = lambda k: np.asarray(sd[k], F32)  # noqa: E731
-        layers, (hw, hb) = layer_keys(n_inner, num_snake, num_tanh)
-        return cls(g("net.0.linear.weight"), g("net.0.linear.bias"), [g(w) for _, w, _, _ in layers],
+        layers, (hw, hb) = layer_keys(n_inner, num_snake, num_tanh, first_linear, last_linear)
+        w0k, b0k, a0k = first_keys(first_linear)
+        return cls(g(w0k), g(b0k), [g(w) for _, w, _, _ in layers],
                    [g(b) for _, _, b, _ in layers], g(hw), g(hb), [k for k, _, _, _ in layers],
-                   [None if a is None else g(a) for _, _, _, a in layers])
+                   [None if a is None else g(a) for _, _, _, a in layers],
+                   None if a0k is None else g(a0k), 0.0 if last_linear else hidden_omega)
 
     def to_state_dict(self) -> dict:
-        layers, (hw, hb) = layer_keys(*self.counts())
-        sd = {"net.0.linear.weight": self.W0, "net.0.linear.bias": self.b0}
+        layers, (hw, hb) = self.keys()
+        w0k, b0k, a0k = first_keys(self.a0 is not None)
+        sd = {w0k: self.W0, b0k: self.b0}
+        if a0k is not None:
+            sd[a0k] = self.a0
         for i, (_, wk, bk, ak) in enumerate(layers):
             sd[wk] = self.W[i]
             sd[bk] = self.b[i]
@@ -174,11 +197,22 @@ def forward(p: Params, t: np.ndarray, omega0: float, omega: float, half: bool = 
             dtype=F32):
     """Returns (out [N], cache).  cache: Y[0..L] (layer outputs), A[0..L] (omega*linear),
     C[0..L] cos of the pre-activations; fp16-rounded where the HIP path stores fp16."""
-    A0 = first_preact(t, p.W0, p.b0, omega0)
-    Y0 = sin32(A0)
+    if p.a0 is None:
+        A0 = first_preact(t, p.W0, p.b0, omega0)
+        Y0 = sin32(A0)
+        C0 = cos32(A0)
+        E0 = None
+    else:  # first_linear: Linear + Snake (models.py:330-333, :241)
+        A0 = first_preact(t, p.W0, p.b0, 1.0)
+        z, av = np.asarray(A0, F64), np.asarray(p.a0, F64)[None, :]
+        s0, c0 = np.sin(av * z), np.cos(av * z)
+        Y0 = (z + s0 * s0 / av).astype(F32)
+        C0 = (1.0 + 2.0 * s0 * c0).astype(F32)
+        E0 = ((z * 2.0 * s0 * c0) / av - s0 * s0 / (av * av)).astype(F32)
+        if half:
+            E0 = f16_round(E0)
     Y = [f16_round(Y0) if half else Y0]
-    C0 = cos32(A0)
-    A, C, E = [A0], [f16_round(C0) if half else C0], [None]
+    A, C, E = [A0], [f16_round(C0) if half else C0], [E0]
     for Wi, bi, kind, ai in zip(p.W, p.b, p.kinds, p.a):
         Wm = f16_round(Wi) if half else Wi
         z = np.asarray(Y[-1], dtype) @ np.asarray(Wm, dtype).T + np.asarray(bi, dtype)
@@ -205,7 +239,10 @@ def forward(p: Params, t: np.ndarray, omega0: float, omega: float, half: bool = 
         C.append(np.asarray(c, dtype if not half else F32))
         E.append(None if e is None else np.asarray(e, dtype if not half else F32))
     out = np.asarray(Y[-1], dtype) @ np.asarray(p.wf, dtype) + dtype(p.bf)
-    return out, {"Y": Y, "A": A, "C": C, "E": E}
+    o_lin = out
+    if p.head_omega:  # last_linear=False: final SineLayer(H, 1)
+        out = np.sin(np.asarray(dtype(p.head_omega) * out, F64)).astype(dtype)
+    return out, {"Y": Y, "A": A, "C": C, "E": E, "o": o_lin}
 
 
 def mse(out: np.ndarray, y: np.ndarray) -> float:
@@ -220,7 +257,10 @@ def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float
     rounded as the HIP path stores it: fp16(dZ_i * S) / S (exact power-of-two scale)."""
     L = len(p.W)
     Y, A, C, E = cache["Y"], cache["A"], cache["C"], cache.get("E", [None] * (L + 1))
-    layers, (hw, hb) = layer_keys(*p.counts())
+    layers, (hw, hb) = p.keys()
+    if p.head_omega:  # through the final sine: dLoss/do = g cos(omega o) omega
+        o = np.asarray(cache["o"], F64)
+        g = (np.asarray(g, F64) * np.cos(p.head_omega * o) * p.head_omega).astype(F32)
     # backward scale bound: |dY/dz| of the last layer (elementwise.hip grad_scale / capi act_bound)
     bound = {"sine": omega, "snake": 2.0, "tanh": 1.0}[p.kinds[-1]]
     S = grad_scale(g, p.wf, bound) if half else 1.0
@@ -245,11 +285,16 @@ def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float
         grads[bk] = db
         Wm = f16_round(p.W[i - 1]) if half else p.W[i - 1]
         dY = dZ @ np.asarray(Wm, dtype)
-    cos0 = np.asarray(C[0], dtype) if half else np.cos(np.asarray(A[0], F64)).astype(dtype)
-    dZ0 = dY * cos0 * dtype(omega0)
+    w0k, b0k, a0k = first_keys(p.a0 is not None)
+    if p.a0 is None:
+        cos0 = np.asarray(C[0], dtype) if half else np.cos(np.asarray(A[0], F64)).astype(dtype)
+        dZ0 = dY * cos0 * dtype(omega0)
+    else:
+        dZ0 = dY * np.asarray(C[0], dtype)
+        grads[a0k] = (dY * np.asarray(E[0], dtype)).sum(0)
     tt = np.asarray(t, dtype).reshape(dZ0.shape[0], -1)
-    grads["net.0.linear.weight"] = dZ0.T @ tt
-    grads["net.0.linear.bias"] = dZ0.sum(0)
+    grads[w0k] = dZ0.T @ tt
+    grads[b0k] = dZ0.sum(0)
     return grads
 
 
@@ -318,7 +363,7 @@ def reported_snr(ref_raw, fs, rec, duration, decimation=1) -> float:
 def fit(p: Params, t, y, omega0, omega, steps, lr=1e-3, min_lr=1e-6, half=False):
     """Full-batch fit with the restated loop; returns (params, losses, lrs)."""
     names = list(p.to_state_dict().keys())
-    counts = p.counts()
+    counts = p.counts() + (p.a0 is not None, p.head_omega == 0, p.head_omega or 30.0)
     flat = [x.astype(F32).copy() for x in p.to_state_dict().values()]
     ms = [np.zeros_like(x) for x in flat]
     vs = [np.zeros_like(x) for x in flat]

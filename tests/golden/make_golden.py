@@ -101,17 +101,20 @@ def act_fixtures(ref_models, ref_utils, steps):
     coords, target = ref_utils.WaveformFitting(wav, duration=1, decimation=1)[0]
     idx = np.arange(0, 44100, 21)
     c_sub, t_sub = coords[idx], target[idx]
-    cfgs = {  # name: (H, num_sine, num_snake, num_tanh, omega0, a_initial, seed)
-        "default": (256, 2, 2, 0, 1000.0, 0.5, 1),
-        "mix": (128, 1, 2, 1, 1000.0, 0.5, 0),
-        "tanh": (128, 1, 0, 2, 1000.0, 0.5, 2),
+    cfgs = {  # name: (H, num_sine, num_snake, num_tanh, omega0, a_initial, seed, first_linear, last_linear)
+        "default": (256, 2, 2, 0, 1000.0, 0.5, 1, False, True),
+        "mix": (128, 1, 2, 1, 1000.0, 0.5, 0, False, True),
+        "tanh": (128, 1, 0, 2, 1000.0, 0.5, 2, False, True),
+        "firstlin": (128, 1, 1, 0, 1000.0, 0.5, 5, True, True),
+        "lastsine": (128, 2, 0, 0, 1000.0, 0.5, 6, False, False),
+        "both": (128, 1, 1, 1, 1000.0, 2.0, 7, True, False),
     }
     fb = {"subset_idx": idx}
-    for name, (H, ns, nk, nt, w0, a0, seed) in cfgs.items():
+    for name, (H, ns, nk, nt, w0, a0, seed, fl, ll) in cfgs.items():
         torch.manual_seed(seed)
         m = ref_models.SirenWithSnakeTanh(in_features=1, out_features=1, hidden_features=H, num_sine=ns,
-                                          num_snake=nk, num_tanh=nt, first_omega_0=w0, hidden_omega_0=30.0,
-                                          a_initial=a0)
+                                          num_snake=nk, num_tanh=nt, first_linear=fl, last_linear=ll,
+                                          first_omega_0=w0, hidden_omega_0=30.0, a_initial=a0)
         for k, v in sd_np(m).items():
             fb[f"{name}_init_{k}"] = v
         out, loss, grads = fwd_bwd(m, c_sub, t_sub)

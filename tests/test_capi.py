@@ -35,7 +35,7 @@ def test_binding_table_matches_header(lib):
 
 
 def test_host_only_helpers(lib):
-    assert lib.siren_abi_version() == 3
+    assert lib.siren_abi_version() == 4
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256

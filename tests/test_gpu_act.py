@@ -184,10 +184,11 @@ def test_head_bwd_snake(lib, dev, H):
 
 
 # ------------------------------------------------------------------ fused step / drop-in
-def _model(H, ns, nk, nt, w0=1000.0, a0=0.5, seed=0, in_dim=1):
+def _model(H, ns, nk, nt, w0=1000.0, a0=0.5, seed=0, in_dim=1, fl=False, ll=True):
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     torch.manual_seed(seed)
-    return SirenWithSnakeTanh(in_dim, 1, H, ns, nk, nt, first_omega_0=w0, hidden_omega_0=30.0, a_initial=a0)
+    return SirenWithSnakeTanh(in_dim, 1, H, ns, nk, nt, first_linear=fl, last_linear=ll, first_omega_0=w0,
+                              hidden_omega_0=30.0, a_initial=a0)
 
 
 def _signal(n, in_dim=1):
@@ -208,17 +209,21 @@ def _rel(a, b):
     (128, (1, 2, 1), 1500, 0.5, 1, 1024),        # sine + Snake + Tanh, 2 micro-batches
     (512, (1, 1, 2), 1000, 5.0, 2, 1 << 20),     # stereo grid, Tanh last
     (1024, (0, 4, 0), 1024, 50.0, 1, 1 << 20),   # the reference's __main__ run (run.py:466)
+    (256, (1, 1, 0, True, True), 1500, 0.5, 1, 1 << 20),    # first_linear: Linear + Snake first
+    (256, (2, 0, 0, False, False), 1500, 0.5, 1, 1 << 20),  # last_linear=False: final SineLayer
+    (256, (1, 1, 1, True, False), 1500, 2.0, 2, 1024),      # both, stereo grid, micro-batches
 ])
 def test_train_step_act_vs_oracle(dev, H, cfg, n, a0, in_dim, mb):
     from inr_for_audio_amd.engine import SirenEngine
-    model = _model(H, *cfg, a0=a0, in_dim=in_dim)
+    fl, ll = (cfg[3], cfg[4]) if len(cfg) > 3 else (False, True)
+    model = _model(H, *cfg[:3], a0=a0, in_dim=in_dim, fl=fl, ll=ll)
     sd0 = {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
     t, y = _signal(n, in_dim)
     eng = SirenEngine(model, t, y, lr=1e-3, micro_batch=mb, device=dev)
     eng.step()
     torch.cuda.synchronize()
     got = {k: v.detach().cpu().numpy() for k, v in zip(eng.layout.names, eng.grad_views())}
-    p = orc.Params.from_state_dict(sd0, *cfg)
+    p = orc.Params.from_state_dict(sd0, *cfg[:3], fl, ll)
     out, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
     ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), 1000.0, 30.0, half=True)
     assert set(ref) == set(got)
@@ -228,16 +233,18 @@ def test_train_step_act_vs_oracle(dev, H, cfg, n, a0, in_dim, mb):
     assert abs(eng.last_loss() - orc.mse(out32, y.numpy())) < 2e-2 * orc.mse(out32, y.numpy())
 
 
-def test_autograd_dropin_act(dev):
-    """model(x) / loss.backward() on the default Snake architecture: HIP forward and backward
-    through _SirenFunction, gradients on every parameter including the Snake a's."""
-    model = _model(256, 2, 2, 0).to(dev)
+@pytest.mark.parametrize("fl,ll", [(False, True), (True, False)])
+def test_autograd_dropin_act(dev, fl, ll):
+    """model(x) / loss.backward() on the default Snake architecture (and with a first
+    Linear+Snake and a final SineLayer): HIP forward and backward through _SirenFunction,
+    gradients on every parameter including the Snake a's."""
+    model = _model(256, 2, 2, 0, fl=fl, ll=ll).to(dev)
     sd0 = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
     t, y = _signal(1500)
     out = model(t.to(dev).reshape(1, -1, 1))
     loss = torch.nn.MSELoss()(out, y.to(dev).reshape(1, -1, 1))
     loss.backward()
-    p = orc.Params.from_state_dict(sd0, 2, 2, 0)
+    p = orc.Params.from_state_dict(sd0, 2, 2, 0, fl, ll)
     o, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
     assert np.max(np.abs(out.detach().cpu().numpy().reshape(-1) - o)) < 2e-2 * np.max(np.abs(o)) + 1e-3
     ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(o, y.numpy()), 1000.0, 30.0, half=True)

@@ -58,8 +58,8 @@ def test_hip_spec_validation():
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     spec = _model(256, 2, 22000.0).hip_spec()
     assert (spec.in_dim, spec.hidden, spec.n_inner, spec.omega0, spec.omega) == (1, 256, 2, 22000.0, 30.0)
-    bad = [dict(first_linear=True), dict(last_linear=False), dict(hidden_features=384),
-           dict(num_sine=0), dict(in_features=3), dict(num_sine=10, num_snake=4, num_tanh=3)]
+    bad = [dict(hidden_features=384), dict(num_sine=0), dict(in_features=3), dict(out_features=2),
+           dict(num_sine=10, num_snake=4, num_tanh=3)]
     for kw in bad:
         args = dict(in_features=1, out_features=1, hidden_features=256, num_sine=2, num_snake=0, num_tanh=0)
         args.update(kw)
