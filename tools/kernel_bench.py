@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--diags", default="", help="SIREN_OPT_NT_DIAG ablation bits to add as extra "
                     "NT cases (1: L2-resident X, 2: no epilogue stores, 3: both); timing only")
     ap.add_argument("--pf-dists", default="2", help="SIREN_OPT_NT_PF_DIST values for NT pipe 5")
+    ap.add_argument("--dw-splits", default="", help="extra dW cases at these split-K counts (256 tile)")
     args = ap.parse_args()
     import __graft_entry__ as ge
     ge.build()
@@ -82,8 +83,9 @@ def main():
 
     slabs = {}
 
-    def run_dw(tile):
-        splits = lib.siren_default_splits(R, H) if tile == 0 else max(1, (512 if tile == 256 else 1024) // ((H // tile) ** 2))
+    def run_dw(tile, splits=None):
+        if splits is None:
+            splits = lib.siren_default_splits(R, H) if tile == 0 else max(1, (512 if tile == 256 else 1024) // ((H // tile) ** 2))
         if splits not in slabs:
             slabs[splits] = torch.empty(int(lib.siren_slab_floats(H, splits)), device=dev)
         return lib.siren_inner_bwd_dw(P(Y), P(dZ), R, H, splits, tile, P(slabs[splits]), s())
@@ -102,6 +104,8 @@ def main():
             sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "")
             cases[f"dw_{sfx}"] = (tile, pipe, (lambda tl=tile: run_dw(tl)), flops)
     cases["first_fwd"] = (0, 1, run_first, 0.0)
+    for sp in [int(x) for x in args.dw_splits.split(",") if x]:
+        cases[f"dw_t256p0_s{sp}"] = (256, 0, (lambda sp=sp: run_dw(256, sp)), flops)
     # library calibration points (hipBLASLt through torch): the same contraction shapes with
     # no epilogue, fp16 and bf16 operands, fp16/bf16 output
     Xb, Wb, dZb = X.to(torch.bfloat16), W.to(torch.bfloat16), dZ.to(torch.bfloat16)
