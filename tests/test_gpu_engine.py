@@ -162,3 +162,34 @@ def test_cpu_tensors_raise(lib):
     model = _model(256, 2, 1000.0)
     with pytest.raises(RuntimeError):
         model(torch.zeros(1, 10, 1))
+
+
+@pytest.mark.parametrize("n", [1, 7, 129])
+def test_tiny_and_ragged_inputs(dev, n):
+    """Fewer coordinates than one 128-row tile (padding rows carry g = 0) and one row past a
+    tile: the fused step still equals the oracle, and KAN (no padding) too."""
+    from inr_for_audio_amd.engine import KanEngine, SirenEngine
+    from inr_for_audio_amd.kan import KAN
+    t, y = _signal(n)
+    m = _model(128, 2, 1000.0)
+    sd0 = _sd(m)
+    eng = SirenEngine(m, t, y, device=dev)
+    eng.step()
+    torch.cuda.synchronize()
+    got = {k: v.detach().cpu().numpy() for k, v in zip(eng.layout.names, eng.grad_views())}
+    p = orc.Params.from_state_dict(sd0, 2)
+    out, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
+    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), 1000.0, 30.0, half=True)
+    for k, r in ref.items():
+        assert _rel(got[k].reshape(r.shape), r) < 2e-2, k
+    torch.manual_seed(0)
+    km = KAN([1, 16, 16, 1])
+    ksd = {k: v.detach().numpy().copy() for k, v in km.state_dict().items()}
+    keng = KanEngine(km, t, y, device=dev)
+    keng.step()
+    torch.cuda.synchronize()
+    kgot = {k: v.detach().cpu().numpy() for k, v in zip(keng.layout.names, keng.grad_views())}
+    kout, xs = orc.kan_forward(ksd, t.numpy(), 3)
+    kref = orc.kan_backward(ksd, xs, orc.mse_grad(kout, y.numpy()), 3)
+    for k, r in kref.items():
+        assert _rel(kgot[k].reshape(r.shape), r) < 1e-4, k
