@@ -77,6 +77,21 @@ def pmc_traffic(kind: str):
     return (2.0 * fetch + write) * 1024.0, os.path.relpath(files[-1], ROOT)
 
 
+def pmc_mfma_util(kind: str):
+    """MFMA utilisation of `kind` at its actual clock from the newest committed
+    profiles/r*/bench_pmc_mfma.json (tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES over the SIMD
+    cycles implied by GRBM_GUI_ACTIVE), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "bench_pmc_mfma.json")))
+    if not files or kind not in KIND_MATCH:
+        return None
+    with open(files[-1]) as f:
+        pmc = json.load(f)
+    a, b = KIND_MATCH[kind]
+    vals = [v["mfma_util"] for k, v in pmc.items() if a in k and b in k]
+    return sum(vals) / len(vals) if vals else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -176,7 +191,8 @@ def main():
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "flops_per_launch": flops_gemm,
                      "hbm_gbs_at_traffic": (traffic / (kernels[dom]["avg_ms"] * 1e-3) / 1e9)
-                     if traffic else None},
+                     if traffic else None,
+                     "mfma_util_at_clock_pmc": pmc_mfma_util(dom) if (H == 1024 and per_gpu == 1 << 20) else None},
         "step_mfma_frac": inner_flops_step / (ms_per_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS,
         "gemm_mfma_frac": inner_flops_step / (gemm_ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS,
         "kernels": kernels,
