@@ -267,7 +267,9 @@ class SirenEngine:
             coords, target = coords[lo:hi], target[lo:hi]
         self.n_total = n_global
         self.n_local = n = coords.shape[0]
-        mb = min(round_up(int(micro_batch), ROW_TILE), round_up(max(n, 1), ROW_TILE))
+        # rows padded to 256 (pad rows carry g = 0): the 256x256 GEMM tiles need M % 256 == 0,
+        # the 128-row minimum of the C-ABI would drop a 3.6 M-row shard to the 128x128 kernels
+        mb = min(round_up(int(micro_batch), 2 * ROW_TILE), round_up(max(n, 1), 2 * ROW_TILE))
         self.rows = mb
         self.n_micro = max(1, -(-n // mb))
         padded = self.n_micro * mb
