@@ -38,6 +38,9 @@ enum siren_status {
 };
 
 int siren_abi_version(void);
+/* sizeof of the ABI structs, for binding checks: 0 siren_net, 1 siren_grads, 2 siren_batch,
+ * 3 siren_opt_state, 4 siren_kan_net, 5 siren_kan_grads, 6 siren_kan_batch (-1: unknown) */
+int64_t siren_struct_size(int32_t which);
 const char* siren_status_string(int status);
 
 /* ---- device-resident optimizer state: torch.optim.Adam + ReduceLROnPlateau ------------

@@ -100,6 +100,7 @@ class SirenKanBatch(ctypes.Structure):
 # suite checks that every symbol the header declares is exported.
 _SIGS = {
     "siren_abi_version": (ctypes.c_int, []),
+    "siren_struct_size": (_i64, [_i32]),
     "siren_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "siren_default_splits": (_i32, [_i32, _i32]),
     "siren_slab_floats": (_i64, [_i32, _i32]),
@@ -145,6 +146,8 @@ _SIGS = {
                                           ctypes.POINTER(_i64)]),
 }
 
+STRUCTS = [SirenNet, SirenGrads, SirenBatch, SirenOptState, SirenKanNet, SirenKanGrads, SirenKanBatch]
+
 PROF_KINDS = ["first_fwd", "inner_fwd", "head", "bwd_dw", "bwd_dx", "bwd_dx0", "reduce", "update"]
 
 
@@ -181,6 +184,9 @@ def load(path: str = LIB_PATH):
         fn.argtypes = args
     if lib.siren_abi_version() != ABI_VERSION:
         raise SirenError(f"libsiren_hip ABI {lib.siren_abi_version()} != expected {ABI_VERSION}")
+    for k, st in enumerate(STRUCTS):
+        if lib.siren_struct_size(k) != ctypes.sizeof(st):
+            raise SirenError(f"{st.__name__}: ctypes size {ctypes.sizeof(st)} != C size {lib.siren_struct_size(k)}")
     _lib = lib
     return lib
 

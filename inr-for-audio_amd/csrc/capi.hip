@@ -132,6 +132,19 @@ extern "C" {
 
 int siren_abi_version(void) { return SIREN_ABI_VERSION; }
 
+int64_t siren_struct_size(int32_t which) {
+  switch (which) {
+    case 0: return sizeof(siren_net);
+    case 1: return sizeof(siren_grads);
+    case 2: return sizeof(siren_batch);
+    case 3: return sizeof(siren_opt_state);
+    case 4: return sizeof(siren_kan_net);
+    case 5: return sizeof(siren_kan_grads);
+    case 6: return sizeof(siren_kan_batch);
+  }
+  return -1;
+}
+
 const char* siren_status_string(int status) {
   switch (status) {
     case SIREN_OK: return "ok";

@@ -34,6 +34,15 @@ def test_binding_table_matches_header(lib):
     assert set(_lib._SIGS) == declared()
 
 
+def test_struct_layouts_match(lib):
+    """ctypes mirrors of the ABI structs have the C sizes (load() also refuses a mismatch)."""
+    import ctypes
+    from inr_for_audio_amd import _lib
+    for k, st in enumerate(_lib.STRUCTS):
+        assert lib.siren_struct_size(k) == ctypes.sizeof(st), st.__name__
+    assert lib.siren_struct_size(99) == -1
+
+
 def test_host_only_helpers(lib):
     assert lib.siren_abi_version() == 4
     assert lib.siren_status_string(0) == b"ok"
