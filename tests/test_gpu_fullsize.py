@@ -1,0 +1,64 @@
+"""The headline configuration itself (SIREN 5x1024, 2^20 coordinates -- BASELINE.json configs[1])
+checked through size-independent properties; the fp64 oracle is far too slow at this size (the
+per-kernel and small-step tests pin the arithmetic against it):
+
+* determinism -- two engines from the same init give bit-identical gradients, loss and updated
+  parameters (every reduction in the step is fixed-order);
+* consistency -- the loss the fused step reports equals the MSE of siren_forward's output for
+  the same weights (train and inference share the forward kernels);
+* linearity of the full-batch gradient -- one 2^20-row micro-batch and two 2^19-row micro-batches
+  accumulate the same gradient (to the fp16 storage of dZ, whose scale is chosen per micro-batch).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+N = 1 << 20
+
+
+def _setup(dev, micro_batch=N, seed=0):
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(seed)
+    m = SirenWithSnakeTanh(1, 1, 1024, 4, 0, 0, first_omega_0=3000.0, hidden_omega_0=30.0)
+    t = torch.linspace(-1, 1, N).reshape(N, 1)
+    y = 0.5 * torch.sin(2300.0 * t) + 0.3 * torch.sin(7100.0 * t + 0.5)
+    return SirenEngine(m, t, y, micro_batch=micro_batch, hist_cap=8, device=dev), t, y
+
+
+def test_fullsize_step_is_deterministic(dev):
+    a, _, _ = _setup(dev)
+    b, _, _ = _setup(dev)
+    for _ in range(2):
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.grads, b.grads)
+    assert torch.equal(a.params, b.params)
+    assert np.array_equal(a.history()[0], b.history()[0])
+
+
+def test_fullsize_loss_matches_inference(dev):
+    eng, t, y = _setup(dev)
+    out = eng.infer(t.to(dev)).double()      # with the initial weights
+    mse = float(((out - y.to(dev).reshape(-1).double()) ** 2).mean())
+    eng.step()
+    torch.cuda.synchronize()
+    loss0 = float(eng.history()[0][0])
+    assert abs(loss0 - mse) <= 1e-5 * mse
+
+
+def test_fullsize_microbatch_linearity(dev):
+    one, _, _ = _setup(dev, micro_batch=N)
+    two, _, _ = _setup(dev, micro_batch=N // 2)
+    assert one.n_micro == 1 and two.n_micro == 2
+    one.step()
+    two.step()
+    torch.cuda.synchronize()
+    g1, g2 = one.grads.double(), two.grads.double()
+    rel = float(torch.linalg.norm(g1 - g2) / torch.linalg.norm(g1))
+    assert rel < 1e-2, rel
+    # the summed squared error rides the same vector: identical forward -> near-identical sum
+    s1, s2 = float(g1[one.layout.sse_offset]), float(g2[two.layout.sse_offset])
+    assert abs(s1 - s2) <= 1e-5 * s1
