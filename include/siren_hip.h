@@ -279,8 +279,8 @@ enum siren_prof_kind {
 };
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
  * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;
- * SIREN_OPT_NT_PIPE = 256x256 NT GEMM variant: -1 per mode (default: 4 for the forward, 1 for
- * dX), 0 BK 64 one tile per block, 1 BK 64 persistent, 2 BK 32 4-slot ring persistent, 3 BK 32 3-slot ring persistent,
+ * SIREN_OPT_NT_PIPE = 256x256 NT GEMM variant: -1 automatic (4, every mode; the Snake / Tanh
+ * modes take 4 or else 1), 0 BK 64 one tile per block, 1 BK 64 persistent, 2 BK 32 4-slot ring persistent, 3 BK 32 3-slot ring persistent,
  * 4 BK 64 persistent with two wave groups in ping-pong, 5 BK 64 persistent with the X operand
  * prefetched into L2 SIREN_OPT_NT_PF_DIST (1..16, default 2) K-steps ahead, 6 / 7 128x256 tiles
  * (4 waves), BK 32 3- / 2-slot ring, persistent with two blocks per CU;

@@ -470,13 +470,23 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         psrc[pc][j] = lr * K + stage_swz<BK>(lr, lane & 7) * 8;
         pdst[pc][j] = ((pc & 1) ? 0u : (unsigned)Cfg::XBYTES) + (unsigned)(lr0 * ROWB);
       }
+    // per-tile operand bases, recomputed only when the issuing tile changes (twice per tile
+    // at most): keeps tile_of's division and the 64-bit products out of the per-phase SALU work
+    int c_t = -1;
+    const h16* c_w = p.W;
+    const h16* c_x = p.X;
     auto issue = [&](int ti, int kt, int slot, auto pcc) -> bool {
       constexpr int PC = decltype(pcc)::value;
       if (ti >= my_tiles) return false;
-      int m0, n0;
-      tile_of(ti, m0, n0);
-      const int xm0 = (p.diag & 1) ? (m0 & (4 * BM - 1)) : m0;
-      const h16* src = ((PC & 1) ? p.X + (size_t)xm0 * K : p.W + (size_t)n0 * K) + kt * BK;
+      if (__builtin_expect(ti != c_t, 0)) {
+        int m0, n0;
+        tile_of(ti, m0, n0);
+        const int xm0 = (p.diag & 1) ? (m0 & (4 * BM - 1)) : m0;
+        c_x = p.X + (size_t)xm0 * K;
+        c_w = p.W + (size_t)n0 * K;
+        c_t = ti;
+      }
+      const h16* src = ((PC & 1) ? c_x : c_w) + kt * BK;
       const char* dst = smem + slot * Cfg::STAGE;
 #pragma unroll
       for (int j = 0; j < 2; ++j) glds16_asm(src + psrc[PC][j], lds_addr(dst + pdst[PC][j]));
@@ -607,7 +617,9 @@ static hipError_t dispatch_act(int mode, bool head, const NtParams& p, hipStream
 // tile per block; 1 = BK 64 persistent (default); 2 = BK 32 4-slot ring persistent;
 // 3 = BK 32 3-slot ring persistent; 4 = BK 64 persistent ping-pong (pingpong_tiles)
 static int g_nt_tile = 0;
-static int g_nt_pipe = -1;  // -1: per mode (FWD: ping-pong 4, DX / DX0: 1; kernel_bench r03)
+static int g_nt_pipe = -1;  // -1: automatic = ping-pong 4 for every mode (kernel_bench r06)
+// Snake / Tanh / first-layer-Snake modes have two 256x256 variants: ping-pong (auto) and 1
+static bool nt_pp() { return g_nt_pipe < 0 || g_nt_pipe == 4; }
 void gemm_nt_set_tile(int tile) { g_nt_tile = tile; }
 void gemm_nt_set_pipe(int v) { g_nt_pipe = v; }
 
@@ -626,7 +638,7 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
     if (!p.Eprev) return hipErrorInvalidValue;
     if (p.tile == 256) {
       if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
-      return dispatch_dx0_snake<NtLarge>(p, s, true);
+      return nt_pp() ? dispatch_dx0_snake<NtLargePP>(p, s, true) : dispatch_dx0_snake<NtLarge>(p, s, true);
     }
     if (p.tile != 128) return hipErrorInvalidValue;
     return dispatch_dx0_snake<NtSmall>(p, s, false);
@@ -636,14 +648,14 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
       return hipErrorInvalidValue;
     if (p.tile == 256) {
       if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
-      return dispatch_act<NtLarge>(mode, head, p, s, true);
+      return nt_pp() ? dispatch_act<NtLargePP>(mode, head, p, s, true) : dispatch_act<NtLarge>(mode, head, p, s, true);
     }
     if (p.tile != 128) return hipErrorInvalidValue;
     return dispatch_act<NtSmall>(mode, head, p, s, false);
   }
   if (p.tile == 256) {
     if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
-    const int pipe = g_nt_pipe >= 0 ? g_nt_pipe : (mode == NT_FWD ? 4 : 1);
+    const int pipe = g_nt_pipe >= 0 ? g_nt_pipe : 4;
     switch (pipe) {
       case 0: return dispatch_mode<NtLarge>(mode, head, p, s, false);
       case 2: return dispatch_mode<NtLargeR4>(mode, head, p, s, true);

@@ -289,6 +289,12 @@ __device__ __forceinline__ void pp_barrier() {
 
 template <int E>
 __device__ __forceinline__ void pp_wait(unsigned hist, bool relaxed) {
+  // steady state (every one of the last 4 phases issued, not a tile's first K-step): one
+  // compare instead of the popcount switch
+  if (__builtin_expect(((hist & 15u) == 15u) & !relaxed, 1)) {
+    wait_vmcnt<8>();
+    return;
+  }
   const int y = __builtin_popcount(hist & 15u);  // pieces issued in phases r-3..r
   if (relaxed) {
     switch (y) {
