@@ -507,7 +507,7 @@ int siren_set_option(int32_t option, int32_t value) {
       return SIREN_OK;
     case SIREN_OPT_NT_PIPE:
     case SIREN_OPT_TN_PIPE:
-      if (value < (option == SIREN_OPT_NT_PIPE ? -1 : 0) || value > (option == SIREN_OPT_NT_PIPE ? 7 : 3))
+      if (value < -1 || value > (option == SIREN_OPT_NT_PIPE ? 7 : 3))
         return SIREN_ERR_CONFIG;
       if (option == SIREN_OPT_NT_PIPE) gemm_nt_set_pipe(value);
       else gemm_tn_set_pipe(value);
@@ -521,7 +521,7 @@ int siren_set_option(int32_t option, int32_t value) {
       gemm_nt_set_pf_dist(value);
       return SIREN_OK;
     case SIREN_OPT_NT_DIAG:
-      if (value < 0 || value > 15) return SIREN_ERR_CONFIG;
+      if (value < 0 || value > 2047) return SIREN_ERR_CONFIG;
       gemm_nt_set_diag(value);
       return SIREN_OK;
     case SIREN_OPT_NT_STAGGER:

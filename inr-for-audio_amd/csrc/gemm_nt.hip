@@ -135,7 +135,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // hold consecutive tile ids, i.e. they share X row-blocks in L2 at the same time.
   const int G = gridDim.x;
   const int bp = xcd_remap(blockIdx.x, G);
-  const int my_tiles = (ntiles - bp + G - 1) / G;
+  const int my_tiles = (p.diag & 512) ? 0 : (ntiles - bp + G - 1) / G;  // diag bit 9: no tiles
   // Start stagger: blocks that run in lockstep hit their epilogues together and their
   // stores then arrive as one chip-wide burst; spreading the starts over a tile's duration
   // spreads the bursts.
@@ -470,27 +470,26 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         psrc[pc][j] = lr * K + stage_swz<BK>(lr, lane & 7) * 8;
         pdst[pc][j] = ((pc & 1) ? 0u : (unsigned)Cfg::XBYTES) + (unsigned)(lr0 * ROWB);
       }
-    // per-tile operand bases, recomputed only when the issuing tile changes (twice per tile
-    // at most): keeps tile_of's division and the 64-bit products out of the per-phase SALU work
-    int c_t = -1;
-    const h16* c_w = p.W;
-    const h16* c_x = p.X;
-    auto issue = [&](int ti, int kt, int slot, auto pcc) -> bool {
-      constexpr int PC = decltype(pcc)::value;
-      if (ti >= my_tiles) return false;
-      if (__builtin_expect(ti != c_t, 0)) {
+    // operand bases of the current tile (0) and the next one (1), set once per tile:
+    // no division or 64-bit product in the per-phase scalar work
+    const h16 *x0 = p.X, *x1 = p.X, *w0 = p.W, *w1 = p.W;
+    auto set_tiles = [&](int ti) {
+      auto bases = [&](int t, const h16*& xb, const h16*& wb) {
         int m0, n0;
-        tile_of(ti, m0, n0);
+        tile_of(t, m0, n0);
         const int xm0 = (p.diag & 1) ? (m0 & (4 * BM - 1)) : m0;
-        c_x = p.X + (size_t)xm0 * K;
-        c_w = p.W + (size_t)n0 * K;
-        c_t = ti;
-      }
-      const h16* src = ((PC & 1) ? c_x : c_w) + kt * BK;
+        xb = p.X + (size_t)xm0 * K;
+        wb = p.W + (size_t)n0 * K;
+      };
+      bases(ti, x0, w0);
+      bases(ti + 1 < my_tiles ? ti + 1 : ti, x1, w1);
+    };
+    auto issue = [&](int sel, int kt, int slot, auto pcc) {
+      constexpr int PC = decltype(pcc)::value;
+      const h16* src = ((PC & 1) ? (sel ? x1 : x0) : (sel ? w1 : w0)) + kt * BK;
       const char* dst = smem + slot * Cfg::STAGE;
 #pragma unroll
       for (int j = 0; j < 2; ++j) glds16_asm(src + psrc[PC][j], lds_addr(dst + pdst[PC][j]));
-      return true;
     };
     h16x8 xf[4][2], wf0[2][2], wf1[2][2];
     auto rd_w = [&](h16x8 (&wf)[2][2], const char* ws, int n_off) {
@@ -530,13 +529,14 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     };
     auto tile_end = [&](int ti) {
       pre(ti);
-      epilogue(ti);
+      if (!(p.diag & 1024)) epilogue(ti);  // diag bit 10: no epilogue (timing only)
 #pragma unroll
       for (int i = 0; i < SN; ++i)
 #pragma unroll
         for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(my_tiles, nk, wm, issue, read, mma, tile_end);
+    pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(my_tiles, nk, wm, issue, read, mma, set_tiles,
+                                                         tile_end);
   } else {
     mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR + Cfg::PF, SN, SM,
                         epilogue_stores<Cfg, MODE>(), Cfg::PF>(
@@ -561,6 +561,8 @@ extern "C" void siren_debug_nt_stamps(void* buf) { g_nt_stamps = (unsigned long 
 
 template <class Cfg, int MODE, bool HEAD>
 static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent) {
+  // the static ping-pong schedule assumes an even number (>= 2) of K-tiles per tile
+  if (Cfg::PP && (p_in.K % (2 * Cfg::BK) != 0 || !persistent)) return hipErrorInvalidValue;
   NtParams p = p_in;
   p.stagger = persistent ? g_nt_stagger : 0;
   p.diag = g_nt_diag;

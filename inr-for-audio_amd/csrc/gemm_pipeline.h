@@ -255,7 +255,7 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
 // (BK = 64) is 4 phases a, b, c, d; each phase is
 //     MEM:  ds_read this phase's fragments; issue one staging piece (16 KiB = 2 LDS-DMA per
 //           wave); [counted vmcnt]
-//     s_barrier; lgkmcnt(0); setprio 1; 16 MFMA; setprio 0; s_barrier
+//     s_barrier; setprio 1; 16 MFMA; lgkmcnt(0); setprio 0; s_barrier
 // Group 1 executes one extra s_barrier first, so group 0's MFMA cluster runs between the same
 // two barrier instances as group 1's MEM section and vice versa.
 //
@@ -268,15 +268,23 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
 //   last ds_read of pc 0 in phase <= a, pc 1 <= b, pc 2 <= c, pc 3 <= d   (WAR)
 //   first ds_read of pc 0, pc 1 >= a (wait in d); pc 2 >= b (wait in a, or in b when first
 //   read in c); pc 3 >= c (wait in b)                                      (RAW)
-// WAITMASK bit PH = phase PH waits.  A wait lets the pieces of phases r-3..r stay in flight
-// (`hist` records which phases issued one), i.e. piece r-4 has landed.  A tile's epilogue
-// (tile_end) issues >= E stores after the pieces then in flight; the waits of the next tile's
-// first K-tile (whose awaited piece is older than those stores) count them as in flight too.
-//   issue(ti, kt, slot, phase_t<PC>) -> bool   LDS-DMA of piece PC of K-step kt of the block's
-//                                   tile ti into LDS slot `slot` (false: ti past the last tile)
-//   read(phase_t<PH>, slot)         this wave's fragments for phase PH
-//   mma(phase_t<PH>)                its 16 MFMAs
-//   tile_end(ti)                    epilogue with both groups aligned (equal barrier count)
+// Static schedule (tiles of an even number nk >= 2 of K-tiles, or one tile per block): every
+// phase issues exactly one piece, so every wait is a compile-time vmcnt and the K-loop has no
+// data-dependent branch.  The pieces a K-step issues belong to K-tiles u+1 and u+2, i.e. to the
+// current tile or the next one, picked by `sel` between two operand bases the caller keeps.
+// Past the block's last tile the issues re-read valid rows into LDS pieces that were already
+// consumed and that nothing reads again; they are drained (vmcnt(0)) before the loop returns.
+// WAITMASK bit PH = phase PH waits: vmcnt(8) keeps the pieces of phases r-3..r in flight, i.e.
+// piece r-4 has landed.  A tile's epilogue (tile_end) issues >= E stores after the pieces then
+// in flight; the waits of the next tile's first K-tile (whose awaited pieces are older than
+// those stores) count them as in flight too: vmcnt(8 + E).
+//   issue(sel, k, slot, phase_t<PC>)  LDS-DMA of piece PC of K-tile k of tile ti + sel into
+//                                     LDS slot `slot`
+//   read(phase_t<PH>, slot)           this wave's fragments for phase PH
+//   mma(phase_t<PH>)                  its 16 MFMAs
+//   set_tiles(ti)                     operand bases of tiles ti and ti + 1 (ti again at the
+//                                     block's last tile)
+//   tile_end(ti)                      epilogue with both groups aligned (equal barrier count)
 template <int PH>
 using phase_t = std::integral_constant<int, PH>;
 
@@ -287,86 +295,58 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int E>
-__device__ __forceinline__ void pp_wait(unsigned hist, bool relaxed) {
-  // steady state (every one of the last 4 phases issued, not a tile's first K-step): one
-  // compare instead of the popcount switch
-  if (__builtin_expect(((hist & 15u) == 15u) & !relaxed, 1)) {
-    wait_vmcnt<8>();
-    return;
-  }
-  const int y = __builtin_popcount(hist & 15u);  // pieces issued in phases r-3..r
-  if (relaxed) {
-    switch (y) {
-      case 4: wait_vmcnt<8 + E>(); break;
-      case 3: wait_vmcnt<6 + E>(); break;
-      case 2: wait_vmcnt<4 + E>(); break;
-      case 1: wait_vmcnt<2 + E>(); break;
-      default: wait_vmcnt<E>(); break;
-    }
-  } else {
-    switch (y) {
-      case 4: wait_vmcnt<8>(); break;
-      case 3: wait_vmcnt<6>(); break;
-      case 2: wait_vmcnt<4>(); break;
-      case 1: wait_vmcnt<2>(); break;
-      default: wait_vmcnt<0>(); break;
-    }
-  }
-}
-
-template <int E, int WAITMASK, class IssueFn, class ReadFn, class MmaFn, class EndFn>
+template <int E, int WAITMASK, class IssueFn, class ReadFn, class MmaFn, class SetFn, class EndFn>
 __device__ __forceinline__ void pingpong_tiles(int ntiles, int nk, int grp, IssueFn&& issue,
-                                               ReadFn&& read, MmaFn&& mma, EndFn&& tile_end) {
+                                                ReadFn&& read, MmaFn&& mma, SetFn&& set_tiles,
+                                                EndFn&& tile_end) {
   static_assert(E >= 0 && 8 + E < 64, "vmcnt immediate");
-  if (ntiles * nk <= 0) return;
-  // (tile, K-step) of the K-tiles u+1 and u+2, advanced incrementally (scalar, no division)
-  auto next = [&](int& t, int& k) {
-    if (++k == nk) { k = 0; ++t; }
-  };
-  int t1 = 0, k1 = 0, t2, k2;
-  next(t1, k1);
-  t2 = t1, k2 = k1;
-  next(t2, k2);
-  unsigned hist = 0;  // bit i: a piece was issued i phases ago
-  hist = (hist << 1) | (unsigned)issue(0, 0, 0, phase_t<0>{});
-  hist = (hist << 1) | (unsigned)issue(0, 0, 0, phase_t<1>{});
-  hist = (hist << 1) | (unsigned)issue(0, 0, 0, phase_t<2>{});
-  hist = (hist << 1) | (unsigned)issue(0, 0, 0, phase_t<3>{});
-  hist = (hist << 1) | (unsigned)issue(t1, k1, 1, phase_t<0>{});
-  hist = (hist << 1) | (unsigned)issue(t1, k1, 1, phase_t<1>{});
-  pp_wait<0>(hist, false);  // this wave's share of K-tile 0's pieces 0, 1 has landed
+  if (ntiles <= 0 || nk <= 0) return;
+  set_tiles(0);
+  issue(0, 0, 0, phase_t<0>{});
+  issue(0, 0, 0, phase_t<1>{});
+  issue(0, 0, 0, phase_t<2>{});
+  issue(0, 0, 0, phase_t<3>{});
+  issue(0, 1, 1, phase_t<0>{});
+  issue(0, 1, 1, phase_t<1>{});
+  wait_vmcnt<8>();  // this wave's share of K-tile 0's pieces 0, 1 has landed
   wait_lgkm0();
-  pp_barrier();             // ... every wave's
-  if (grp) pp_barrier();    // group 1 runs one barrier behind
-  int u = 0;
+  pp_barrier();           // ... every wave's
+  if (grp) pp_barrier();  // group 1 runs one barrier behind
+  // one K-step (4 phases) of K-tile kt in LDS slot kt & 1; RELAXED: the tile's first K-step
+  // after an epilogue whose E stores sit between the awaited pieces and the newest ones
+  auto kstep = [&](int kt, auto relaxed) {
+    constexpr bool RELAXED = decltype(relaxed)::value;
+    const int slot = kt & 1;
+    int ka = kt + 1, kb = kt + 2;
+    const int sa = ka >= nk, sb = kb >= nk;
+    ka -= sa ? nk : 0;
+    kb -= sb ? nk : 0;
+    auto phase = [&](auto ph) {
+      constexpr int PH = decltype(ph)::value;
+      read(ph, slot);
+      if constexpr (PH < 2) issue(sa, ka, slot ^ 1, phase_t<PH + 2>{});
+      else issue(sb, kb, slot, phase_t<PH - 2>{});
+      if constexpr (((WAITMASK >> PH) & 1) != 0) wait_vmcnt<RELAXED ? 8 + E : 8>();
+      pp_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      mma(ph);       // each MFMA waits (counted lgkmcnt) only for its fragments
+      wait_lgkm0();  // every read of this slot has landed before the barrier that frees it
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    };
+    phase(phase_t<0>{});
+    phase(phase_t<1>{});
+    phase(phase_t<2>{});
+    phase(phase_t<3>{});
+  };
   for (int ti = 0; ti < ntiles; ++ti) {
-    for (int kt = 0; kt < nk; ++kt, ++u) {
-      const bool relaxed = (kt == 0) && (ti > 0);
-      const int slot = u & 1;
-      auto phase = [&](auto ph) {
-        constexpr int PH = decltype(ph)::value;
-        read(ph, slot);
-        if constexpr (PH < 2) hist = (hist << 1) | (unsigned)issue(t1, k1, slot ^ 1, phase_t<PH + 2>{});
-        else hist = (hist << 1) | (unsigned)issue(t2, k2, slot, phase_t<PH - 2>{});
-        if constexpr (((WAITMASK >> PH) & 1) != 0) pp_wait<E>(hist, relaxed);
-        pp_barrier();
-        wait_lgkm0();
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        mma(ph);
-        __builtin_amdgcn_s_setprio(0);
-        pp_barrier();
-      };
-      phase(phase_t<0>{});
-      phase(phase_t<1>{});
-      phase(phase_t<2>{});
-      phase(phase_t<3>{});
-      t1 = t2, k1 = k2;
-      next(t2, k2);
-    }
+    if (ti == 0) kstep(0, std::false_type{});
+    else kstep(0, std::true_type{});
+    for (int kt = 1; kt < nk; ++kt) kstep(kt, std::false_type{});
     if (grp == 0) pp_barrier();                     // meet group 1's last barrier: aligned
     tile_end(ti);
+    if (ti + 1 < ntiles) set_tiles(ti + 1);
     if (grp == 1 && ti + 1 < ntiles) pp_barrier();  // group 1 one barrier behind again
   }
   wait_vmcnt<0>();

@@ -151,10 +151,11 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
         po[kk][j] = (unsigned)(r0 * YROW);
       }
     const int nkl = ks_end - ks_begin;
-    auto issue = [&](int ti, int kt, int slot, auto pcc) -> bool {
+    // one tile per block: pieces addressed past it (sel = 1, or past the slice's last K-step)
+    // re-read a valid K-step into LDS pieces already consumed (pingpong_tiles contract)
+    auto issue = [&](int sel, int kt, int slot, auto pcc) {
       constexpr int PC = decltype(pcc)::value, KK = PC >> 1;
-      if (ti > 0) return false;
-      const int ks = ks_begin + kt;
+      const int ks = ks_begin + min(sel ? 0 : kt, nkl - 1);
       const char* dst = smem + slot * Cfg::STAGE;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -163,7 +164,6 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
         else
           glds16_asm(p.dZ + (size_t)ks * BK * p.Hout + zo[KK][j], lds_addr(dst + Cfg::YBYTES + po[KK][j]));
       }
-      return true;
     };
     h16x8 af[4], bf[4];
     auto read = [&](auto ph, int slot) {
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
           acc[4 * IH + il][j] =
               __builtin_amdgcn_mfma_f32_16x16x32_f16(af[il], bf[j], acc[4 * IH + il][j], 0, 0, 0);
     };
-    pingpong_tiles<0, 0xA>(1, nkl, wm, issue, read, mma, [](int) {});
+    pingpong_tiles<0, 0xA>(1, nkl, wm, issue, read, mma, [](int) {}, [](int) {});
   } else {
     mfma_pipeline<Cfg::S, false, BK / 32, Cfg::YINSTR + Cfg::ZINSTR>(ks_end - ks_begin, acc, stage, frags);
   }
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
 }
 
 static int g_tn_tile = 0;
-static int g_tn_pipe = 0;  // BK 64 double buffer: fastest measured (r01 A/B)
+static int g_tn_pipe = -1;  // -1: automatic = 3, BK 64 ping-pong (fastest, kernel_bench r06)
 void gemm_tn_set_tile(int tile) { g_tn_tile = tile; }
 void gemm_tn_set_pipe(int v) { g_tn_pipe = v; }
 
@@ -226,7 +226,7 @@ hipError_t gemm_tn_dw(const TnParams& p, hipStream_t s) {
   if (p.Hin % 128 || p.Hout % 128 || p.R % 64 || p.R <= 0 || p.splits < 1) return hipErrorInvalidValue;
   if (p.tile == 256) {
     if (p.Hin % 256 || p.Hout % 256) return hipErrorInvalidValue;
-    switch (g_tn_pipe) {
+    switch (g_tn_pipe >= 0 ? g_tn_pipe : 3) {
       case 0: return launch_tn<TnL0>(p, s);
       case 1: return (p.R % 32) ? hipErrorInvalidValue : launch_tn<TnL1>(p, s);
       case 2: return launch_tn<TnL2>(p, s);

@@ -10,8 +10,11 @@ summation order on the same seed moves it by as much -- DESIGN.md "Fit parity").
   * fit quality is compared as statistics over init seeds 0-7 against the reference's
     own runs of the same seeds: the median over seeds of the best-loss SNR
     10 log10(var(target) / min_k loss_k) -- the error floor each run reaches, insensitive
-    to where a spike happens to fall -- within 0.5 dB, and the median final SNR within a
-    wide 6 dB band (its seed-to-seed spread is ~10 dB).
+    to where a spike happens to fall -- within 0.5 dB.  The final SNR is a much noisier
+    statistic: bootstrapping the reference's 8 seeds gives its median a 5.5 dB standard
+    deviation (7.8 dB for a difference of two such medians), so it is only checked one-sided
+    at two standard deviations, GPU median >= reference median - 15 dB (a broken optimiser,
+    not spike timing).
 """
 import json
 import os
@@ -73,4 +76,4 @@ def test_fit_quality_vs_reference_over_seeds(dev):
           f"\nper seed GPU  best {np.round(best_gpu, 2).tolist()} final {np.round(fin_gpu, 2).tolist()}"
           f"\nper seed ref  best {np.round(best_ref, 2).tolist()} final {np.round(fin_ref, 2).tolist()}")
     assert abs(med(best_gpu) - med(best_ref)) < 0.5
-    assert abs(med(fin_gpu) - med(fin_ref)) < 6.0
+    assert med(fin_gpu) >= med(fin_ref) - 15.0

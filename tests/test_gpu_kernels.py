@@ -71,7 +71,7 @@ def nt_tile(request, lib):
 def tn_pipe(request, lib):
     ok(lib.siren_set_option(3, request.param), lib)
     yield request.param
-    lib.siren_set_option(3, 0)
+    lib.siren_set_option(3, -1)
 
 
 def _skip_tile(tile, R, H):

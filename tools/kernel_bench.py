@@ -146,8 +146,8 @@ def main():
                 torch.cuda.synchronize()
                 times[name].append(ev0.elapsed_time(ev1) / args.reps)
                 continue
-            lib.siren_set_option(5, stagger[name])
-            lib.siren_set_option(6, diag.get(name, 0))
+            _lib.check(lib.siren_set_option(5, stagger[name]), "stagger option")
+            _lib.check(lib.siren_set_option(6, diag.get(name, 0)), "diag option")
             if pfd.get(name, 0):
                 lib.siren_set_option(7, pfd[name])
             lib.siren_set_option(0, tile if not name.startswith("dw") else 0)
@@ -168,7 +168,7 @@ def main():
     lib.siren_set_option(6, 0)
     lib.siren_set_option(0, 0)
     lib.siren_set_option(2, -1)
-    lib.siren_set_option(3, 0)
+    lib.siren_set_option(3, -1)
     out = {}
     for name, (tile, pipe, fn, fl) in cases.items():
         ts = sorted(times[name])
