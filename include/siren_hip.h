@@ -289,10 +289,10 @@ enum siren_prof_kind {
  * SIREN_OPT_NT_GRID = persistent NT grid size (0 = one block per CU; tests use small
  * values so every block walks several tiles);
  * SIREN_OPT_NT_DIAG = measurement-only NT ablations (results are WRONG while set): bit 0 reads
- *   the X operand from the first 4 row bands only (L2-resident operand), bit 1 drops the
- *   epilogue's global stores (values kept live), bit 2 replaces the forward's sin / cos by
- *   the identity, bit 3 makes the epilogue stores non-temporal; ping-pong K-loop (pipe 4)
- *   only: bit 9 runs no tiles, bit 10 skips the epilogue;
+ *   the X operand from the first 4 row bands only (L2-resident operand); ping-pong K-loop
+ *   (pipe 4) only: bit 9 runs no tiles, bit 10 skips the epilogue (its compute and stores).
+ *   (Bits 1-3 -- no stores, identity sin/cos, non-temporal stores -- were retired in r06: their
+ *   per-store branches cost the production epilogue; DESIGN.md keeps their measurements);
  * SIREN_OPT_NT_STAGGER = persistent NT start stagger: block b idles (b % 16) * value units of
  * ~1.7k cycles before its first tile, so that the blocks' epilogue store bursts do not
  * coincide (0 = none; 0..64). */

@@ -220,14 +220,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   float* red = (float*)(smem + Cfg::RING);
   // 16-B epilogue store; SIREN_OPT_NT_DIAG bit 1 (measurement only) keeps the value live
   // and drops the store
-  auto st16 = [&](h16* dst, uint4 v) {
-    if (p.diag & 2) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-    else if (p.diag & 8) {
-      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-      __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (u32x4*)dst);
-    }
-    else *(uint4*)dst = v;
-  };
+  auto st16 = [&](h16* dst, uint4 v) { *(uint4*)dst = v; };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
   float* bias_lds = (float*)(smem + Lay::BIAS);
@@ -305,13 +298,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                 // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
                 // hardware sin/cos inside their reduced domain for any magnitude.
                 const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
-                if (p.diag & 4) {  // measurement only: no transcendentals
-                  s[r] = x;
-                  c[r] = x;
-                } else {
-                  s[r] = __builtin_amdgcn_sinf(x);
-                  c[r] = __builtin_amdgcn_cosf(x);
-                }
+                s[r] = __builtin_amdgcn_sinf(x);
+                c[r] = __builtin_amdgcn_cosf(x);
               }
             } else if constexpr (MODE == NT_FWD_SNAKE) {
               const float4 a4 = *(const float4*)(a_lds + nq + i * 16);

@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--staggers", default="", help="SIREN_OPT_NT_STAGGER values to add as "
                     "extra persistent NT cases")
     ap.add_argument("--diags", default="", help="SIREN_OPT_NT_DIAG ablation bits to add as extra "
-                    "NT cases (1: L2-resident X, 2: no epilogue stores, 3: both); timing only")
+                    "NT cases (1: L2-resident X; pipe 4: 512 no tiles, 1024 no epilogue); timing only")
     ap.add_argument("--pf-dists", default="2", help="SIREN_OPT_NT_PF_DIST values for NT pipe 5")
     ap.add_argument("--dw-splits", default="", help="extra dW cases at these split-K counts (256 tile)")
     args = ap.parse_args()
