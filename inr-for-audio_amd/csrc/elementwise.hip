@@ -251,52 +251,59 @@ hipError_t grad_scale(const float* gmax_part, int nparts, const float* w_head, i
 // A Snake / Tanh last layer passes its derivative as C with omega = 1; a Snake one also E
 // (dY/da) and gets da partial = sum_m dY[m][n]*E[m][n].
 // The partials are unscaled; the stored dZ carries the gradient scale S (grad_scale).
-__global__ void head_bwd_kernel(const h16* __restrict__ C, const h16* __restrict__ Y,
-                                const float* __restrict__ g, const float* __restrict__ w_head,
-                                float omega, int R, int H, const float* __restrict__ gscale,
-                                h16* __restrict__ dZ, float* __restrict__ db_part,
-                                float* __restrict__ dwh_part, const h16* __restrict__ E,
-                                float* __restrict__ da_part) {
-  __shared__ float red[3][256 * 4];
+template <int V>  // columns per thread: 8 (16-B loads) when H allows, else 4
+__global__ __launch_bounds__(256) void head_bwd_kernel(
+    const h16* __restrict__ C, const h16* __restrict__ Y, const float* __restrict__ g,
+    const float* __restrict__ w_head, float omega, int R, int H, const float* __restrict__ gscale,
+    h16* __restrict__ dZ, float* __restrict__ db_part, float* __restrict__ dwh_part,
+    const h16* __restrict__ E, float* __restrict__ da_part) {
+  typedef _Float16 hv __attribute__((ext_vector_type(V)));
+  __shared__ float red[3][256 * V];
   const float S = gscale ? gscale[0] : 1.0f;  // dZ storage scale (grad_scale)
-  const int hq = H >> 2;            // column quads (divides 256)
+  const int hq = H / V;                        // column groups (divides 256)
   const int cq = threadIdx.x % hq, rg = threadIdx.x / hq, nrg = blockDim.x / hq;
-  const int n = cq * 4;
-  const float4 w = *(const float4*)(w_head + n);
-  const float wv[4] = {w.x, w.y, w.z, w.w};
-  float db[4] = {0.f, 0.f, 0.f, 0.f}, dw[4] = {0.f, 0.f, 0.f, 0.f}, da[4] = {0.f, 0.f, 0.f, 0.f};
+  const int n = cq * V;
+  float wv[V], db[V], dw[V], da[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    wv[k] = w_head[n + k];
+    db[k] = dw[k] = da[k] = 0.f;
+  }
   const int64_t m0 = (int64_t)blockIdx.x * 128;
+  // rows rg, rg + nrg, ...: unrolled so that several rows' loads are in flight per thread
+#pragma unroll 4
   for (int r = rg; r < 128; r += nrg) {
     const int64_t m = m0 + r;
     const float gm = g[m];
-    const h16x4 c = *(const h16x4*)(C + m * H + n);
-    const h16x4 yv = *(const h16x4*)(Y + m * H + n);
-    h16x4 ev = {};
-    if (E) ev = *(const h16x4*)(E + m * H + n);
-    float dz[4];
+    const hv c = *(const hv*)(C + m * H + n);
+    const hv yv = *(const hv*)(Y + m * H + n);
+    hv ev = {};
+    if (E) ev = *(const hv*)(E + m * H + n);
+    hv out;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      dz[k] = ((gm * wv[k]) * (float)c[k]) * omega;
-      db[k] += dz[k];
+    for (int k = 0; k < V; ++k) {
+      const float dz = ((gm * wv[k]) * (float)c[k]) * omega;
+      db[k] += dz;
       dw[k] += gm * (float)yv[k];
       da[k] += (gm * wv[k]) * (float)ev[k];
+      out[k] = (_Float16)(dz * S);
     }
-    *(h16x4*)(dZ + m * H + n) = pack4(dz[0] * S, dz[1] * S, dz[2] * S, dz[3] * S);
+    *(hv*)(dZ + m * H + n) = out;
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    red[0][threadIdx.x * 4 + k] = db[k];
-    red[1][threadIdx.x * 4 + k] = dw[k];
-    red[2][threadIdx.x * 4 + k] = da[k];
+  for (int k = 0; k < V; ++k) {
+    red[0][threadIdx.x * V + k] = db[k];
+    red[1][threadIdx.x * V + k] = dw[k];
+    red[2][threadIdx.x * V + k] = da[k];
   }
   __syncthreads();
   for (int c = threadIdx.x; c < H; c += blockDim.x) {
-    const int q = c >> 2, k = c & 3;
+    const int q = c / V, k = c % V;
     float a = 0.f, b = 0.f, d = 0.f;
     for (int gi = 0; gi < nrg; ++gi) {
-      a += red[0][(gi * hq + q) * 4 + k];
-      b += red[1][(gi * hq + q) * 4 + k];
-      d += red[2][(gi * hq + q) * 4 + k];
+      a += red[0][(gi * hq + q) * V + k];
+      b += red[1][(gi * hq + q) * V + k];
+      d += red[2][(gi * hq + q) * V + k];
     }
     db_part[(size_t)blockIdx.x * H + c] = a;
     dwh_part[(size_t)blockIdx.x * H + c] = b;
@@ -308,8 +315,12 @@ hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_h
                     int R, int H, const float* gscale, h16* dZ, float* db_part, float* dwh_part,
                     const h16* E, float* da_part, hipStream_t s) {
   if (R % 128 || H % 4 || 256 % (H / 4) || (E && !da_part)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(R / 128), dim3(256), 0, s, C, Y, g, w_head, omega, R, H,
-                     gscale, dZ, db_part, dwh_part, E, da_part);
+  if (H % 8 == 0 && 256 % (H / 8) == 0)
+    hipLaunchKernelGGL(head_bwd_kernel<8>, dim3(R / 128), dim3(256), 0, s, C, Y, g, w_head, omega, R, H,
+                       gscale, dZ, db_part, dwh_part, E, da_part);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<4>, dim3(R / 128), dim3(256), 0, s, C, Y, g, w_head, omega, R, H,
+                       gscale, dZ, db_part, dwh_part, E, da_part);
   return hipGetLastError();
 }
 
