@@ -64,15 +64,19 @@ def _release():
     _KEEP.clear()
 
 
-@pytest.fixture(params=[(128, 0), (256, 0), (256, 2)], ids=lambda p: f"t{p[0]}g{p[1]}")
+@pytest.fixture(params=[(128, 0, -1), (256, 0, -1), (256, 2, -1), (256, 0, 1), (256, 2, 1)],
+                ids=lambda p: f"t{p[0]}g{p[1]}p{p[2]}")
 def tile(request, lib):
-    """NT tile edge and persistent grid (grid 2: every block walks several tiles)."""
-    t, grid = request.param
+    """NT tile edge, persistent grid (grid 2: every block walks several tiles) and 256x256
+    K-loop (-1: the automatic ping-pong, 1: the persistent double buffer)."""
+    t, grid, pipe = request.param
     ok(lib.siren_set_option(0, t), lib)
     ok(lib.siren_set_option(4, grid), lib)
+    ok(lib.siren_set_option(2, pipe), lib)
     yield t
     lib.siren_set_option(0, 0)
     lib.siren_set_option(4, 0)
+    lib.siren_set_option(2, -1)
 
 
 def _inputs(rng, R, H):
