@@ -284,8 +284,9 @@ enum siren_prof_kind {
  * 4 BK 64 persistent with two wave groups in ping-pong, 5 BK 64 persistent with the X operand
  * prefetched into L2 SIREN_OPT_NT_PF_DIST (1..16, default 2) K-steps ahead, 6 / 7 128x256 tiles
  * (4 waves), BK 32 3- / 2-slot ring, persistent with two blocks per CU;
- * SIREN_OPT_TN_PIPE = -1..3 selects the 256x256 dW K-loop (-1 automatic = 3; 0: BK 64 double
- * buffer, 1: BK 32 4-slot ring, 2: BK 32 5-slot ring, 3: BK 64 ping-pong);
+ * SIREN_OPT_TN_PIPE = -1..4 selects the 256x256 dW K-loop (-1 automatic = 4; 0: BK 64 double
+ * buffer, 1: BK 32 4-slot ring, 2: BK 32 5-slot ring, 3: BK 64 ping-pong in 16-MFMA phases,
+ * 4: BK 64 ping-pong in 32-MFMA segments);
  * SIREN_OPT_NT_GRID = persistent NT grid size (0 = one block per CU; tests use small
  * values so every block walks several tiles);
  * SIREN_OPT_NT_DIAG = measurement-only NT ablations (results are WRONG while set): bit 0 reads

@@ -507,7 +507,7 @@ int siren_set_option(int32_t option, int32_t value) {
       return SIREN_OK;
     case SIREN_OPT_NT_PIPE:
     case SIREN_OPT_TN_PIPE:
-      if (value < -1 || value > (option == SIREN_OPT_NT_PIPE ? 7 : 3))
+      if (value < -1 || value > (option == SIREN_OPT_NT_PIPE ? 7 : 4))
         return SIREN_ERR_CONFIG;
       if (option == SIREN_OPT_NT_PIPE) gemm_nt_set_pipe(value);
       else gemm_tn_set_pipe(value);

@@ -352,4 +352,53 @@ __device__ __forceinline__ void pingpong_tiles(int ntiles, int nk, int grp, Issu
   wait_vmcnt<0>();
 }
 
+// Two-segment variant (one tile per block, e.g. the split-K dW GEMM): a K-tile is two segments
+// of 32 MFMAs instead of four phases of 16, halving the barriers.  Segment A reads pieces
+// 0 .. NA-1 of K-tile u and issues pieces NA..3 of u+1 into the other slot; segment B reads
+// pieces NA..3 of u and issues pieces 0 .. NA-1 of u+2 into this slot.  Each piece is 2 LDS-DMA
+// per wave, so every wait is vmcnt(8) (the 4 pieces issued since the awaited ones).  A MEM
+// section retires its own reads (lgkmcnt(0)) before its barrier: the other group overwrites
+// those pieces one barrier later.  issue(k, slot, phase_t<PC>), read / mma(phase_t<SEG>).
+template <int NA, class IssueFn, class ReadFn, class MmaFn>
+__device__ __forceinline__ void pingpong2_one_tile(int nk, int grp, IssueFn&& issue, ReadFn&& read,
+                                                   MmaFn&& mma) {
+  static_assert(NA >= 1 && NA <= 3, "pieces per segment");
+  if (nk <= 0) return;
+  auto issue_range = [&](int k, int slot, auto lo, auto hi) {
+    constexpr int LO = decltype(lo)::value, HI = decltype(hi)::value;
+    if constexpr (LO < HI) {
+      issue(k, slot, phase_t<LO>{});
+      if constexpr (LO + 1 < HI) issue(k, slot, phase_t<LO + 1>{});
+      if constexpr (LO + 2 < HI) issue(k, slot, phase_t<LO + 2>{});
+    }
+  };
+  issue_range(0, 0, phase_t<0>{}, phase_t<NA>{});
+  issue_range(0, 0, phase_t<NA>{}, phase_t<4>{});
+  issue_range(1, 1, phase_t<0>{}, phase_t<NA>{});
+  wait_vmcnt<8>();  // this wave's share of K-tile 0's A pieces has landed
+  pp_barrier();
+  if (grp) pp_barrier();  // group 1 runs one barrier behind
+  for (int kt = 0; kt < nk; ++kt) {
+    const int slot = kt & 1;
+    auto segment = [&](auto sg) {
+      constexpr int SG = decltype(sg)::value;
+      read(sg, slot);
+      if constexpr (SG == 0) issue_range(kt + 1, slot ^ 1, phase_t<NA>{}, phase_t<4>{});
+      else issue_range(kt + 2, slot, phase_t<0>{}, phase_t<NA>{});
+      wait_vmcnt<8>();
+      wait_lgkm0();
+      pp_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      mma(sg);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    };
+    segment(phase_t<0>{});
+    segment(phase_t<1>{});
+  }
+  if (grp == 0) pp_barrier();  // both groups end on the same barrier count
+  wait_vmcnt<0>();
+}
+
 }  // namespace siren

@@ -19,10 +19,10 @@
 
 namespace siren {
 
-template <int BI_, int BJ_, int WM_, int WN_, int BK_ = 64, int S_ = 2, bool PP_ = false>
+template <int BI_, int BJ_, int WM_, int WN_, int BK_ = 64, int S_ = 2, int PP_ = 0>
 struct TnCfg {
   static constexpr int BI = BI_, BJ = BJ_, BK = BK_, S = S_;
-  static constexpr bool PP = PP_;  // ping-pong K-loop (gemm_pipeline.h pingpong_tiles)
+  static constexpr int PP = PP_;  // ping-pong K-loop: 1 pingpong_tiles, 2 pingpong2_one_tile
   static constexpr int WM = WM_, WN = WN_, NWAVES = WM_ * WN_, THREADS = 64 * NWAVES;
   static constexpr int TI = BI / WM, TJ = BJ / WN, SI = TI / 16, SJ = TJ / 16;
   static constexpr int YROW = BI * 2, ZROW = BJ * 2;       // bytes per staged row
@@ -38,7 +38,8 @@ using TnLarge = TnCfg<256, 256, 2, 4>;          // slab geometry of every 256x25
 using TnL0 = TnCfg<256, 256, 2, 4, 64, 2>;      // BK 64, double buffer
 using TnL1 = TnCfg<256, 256, 2, 4, 32, 4>;      // BK 32, 4-slot ring
 using TnL2 = TnCfg<256, 256, 2, 4, 32, 5>;      // BK 32, 5-slot ring
-using TnLPP = TnCfg<256, 256, 2, 4, 64, 2, true>;  // BK 64, two wave groups in ping-pong
+using TnLPP = TnCfg<256, 256, 2, 4, 64, 2, 1>;  // BK 64, two wave groups in ping-pong
+using TnLPP2 = TnCfg<256, 256, 2, 4, 64, 2, 2>;  // the same, two 32-MFMA segments per K-tile
 
 // Chunk swizzle of a staged [64][cols] image: physical 16-B chunk = c ^ f(r).  With
 // h(r) = (r&3) | ((r>>3)&1)<<2 and f = 2h, the 8 rows a 32-lane half touches in one
@@ -165,6 +166,39 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
           glds16_asm(p.dZ + (size_t)ks * BK * p.Hout + zo[KK][j], lds_addr(dst + Cfg::YBYTES + po[KK][j]));
       }
     };
+    if constexpr (Cfg::PP == 2) {
+      // segment A = k32 half 0 (pieces 0, 1), B = half 1 (pieces 2, 3); all 8 i-subtiles each
+      h16x8 a8[8], b4[4];
+      auto issue2 = [&](int kt, int slot, auto pcc) {
+        constexpr int PC = decltype(pcc)::value, KK = PC >> 1;
+        const int ks = ks_begin + min(kt, nkl - 1);  // past the slice: a consumed piece re-read
+        const char* dst = smem + slot * Cfg::STAGE;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if constexpr ((PC & 1) != 0)
+            glds16_asm(p.Y + (size_t)ks * BK * p.Hin + yo[KK][j], lds_addr(dst + po[KK][j]));
+          else
+            glds16_asm(p.dZ + (size_t)ks * BK * p.Hout + zo[KK][j], lds_addr(dst + Cfg::YBYTES + po[KK][j]));
+        }
+      };
+      auto read2 = [&](auto sg, int slot) {
+        constexpr int KK = decltype(sg)::value;
+        const char* ys = smem + slot * Cfg::STAGE;
+        const char* zs = ys + Cfg::YBYTES;
+#pragma unroll
+        for (int il = 0; il < 8; ++il) a8[il] = tr_frag<YROW>(ys + KK * 32 * YROW + colA[il]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b4[j] = tr_frag<ZROW>(zs + KK * 32 * ZROW + colB[j]);
+      };
+      auto mma2 = [&](auto sg) {
+#pragma unroll
+        for (int il = 0; il < 8; ++il)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[il][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8[il], b4[j], acc[il][j], 0, 0, 0);
+      };
+      pingpong2_one_tile<2>(nkl, wm, issue2, read2, mma2);
+    } else {
     h16x8 af[4], bf[4];
     auto read = [&](auto ph, int slot) {
       constexpr int PH = decltype(ph)::value, KK = PH >> 1, IH = (PH == 1 || PH == 2) ? 1 : 0;
@@ -187,6 +221,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
               __builtin_amdgcn_mfma_f32_16x16x32_f16(af[il], bf[j], acc[4 * IH + il][j], 0, 0, 0);
     };
     pingpong_tiles<0, 0xA>(1, nkl, wm, issue, read, mma, [](int) {}, [](int) {});
+    }
   } else {
     mfma_pipeline<Cfg::S, false, BK / 32, Cfg::YINSTR + Cfg::ZINSTR>(ks_end - ks_begin, acc, stage, frags);
   }
@@ -202,7 +237,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
 }
 
 static int g_tn_tile = 0;
-static int g_tn_pipe = -1;  // -1: automatic = 3, BK 64 ping-pong (fastest, kernel_bench r06)
+static int g_tn_pipe = -1;  // -1: automatic = 4, two-segment ping-pong (fastest, kernel_bench r06)
 void gemm_tn_set_tile(int tile) { g_tn_tile = tile; }
 void gemm_tn_set_pipe(int v) { g_tn_pipe = v; }
 
@@ -226,11 +261,12 @@ hipError_t gemm_tn_dw(const TnParams& p, hipStream_t s) {
   if (p.Hin % 128 || p.Hout % 128 || p.R % 64 || p.R <= 0 || p.splits < 1) return hipErrorInvalidValue;
   if (p.tile == 256) {
     if (p.Hin % 256 || p.Hout % 256) return hipErrorInvalidValue;
-    switch (g_tn_pipe >= 0 ? g_tn_pipe : 3) {
+    switch (g_tn_pipe >= 0 ? g_tn_pipe : 4) {
       case 0: return launch_tn<TnL0>(p, s);
       case 1: return (p.R % 32) ? hipErrorInvalidValue : launch_tn<TnL1>(p, s);
       case 2: return launch_tn<TnL2>(p, s);
       case 3: return launch_tn<TnLPP>(p, s);
+      case 4: return launch_tn<TnLPP2>(p, s);
     }
     return hipErrorInvalidValue;
   }

@@ -67,7 +67,7 @@ def nt_tile(request, lib):
     lib.siren_set_option(4, 0)
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=lambda p: f"p{p}")
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=lambda p: f"p{p}")
 def tn_pipe(request, lib):
     ok(lib.siren_set_option(3, request.param), lib)
     yield request.param
