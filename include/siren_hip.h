@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 4
+#define SIREN_ABI_VERSION 5
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 
@@ -39,7 +39,8 @@ enum siren_status {
 
 int siren_abi_version(void);
 /* sizeof of the ABI structs, for binding checks: 0 siren_net, 1 siren_grads, 2 siren_batch,
- * 3 siren_opt_state, 4 siren_kan_net, 5 siren_kan_grads, 6 siren_kan_batch (-1: unknown) */
+ * 3 siren_opt_state, 4 siren_kan_net, 5 siren_kan_grads, 6 siren_kan_batch, 7 siren_guard
+ * (-1: unknown) */
 int64_t siren_struct_size(int32_t which);
 const char* siren_status_string(int status);
 
@@ -53,6 +54,24 @@ typedef struct siren_opt_state {
   int32_t patience, pad0;
   double beta1, beta2, eps;
 } siren_opt_state;
+
+/* ---- fp16 backward range guard (device-resident, optional) ---------------------------
+ * The backward stores dZ in fp16 times a power-of-two scale S (siren_grad_scale) chosen so
+ * that the head's bound lands under 2^headroom.  siren_apply_update checks the reduced fp32
+ * gradients: if any is non-finite while the loss is finite (an fp16 overflow of dZ*S, which
+ * fp32 autograd in the reference never has), the Adam and scheduler updates are SKIPPED
+ * (nothing advances: no step, no history entry), headroom drops by 4, and the caller's next
+ * step recomputes the same gradients with a 16x smaller S -- GradScaler-style, but with no
+ * optimizer step lost.  After 1000 clean steps headroom grows back by 1 (up to its initial
+ * value).  Zero-initialise it and set headroom = 6 (the fixed value used when NULL). */
+typedef struct siren_guard {
+  int32_t flag;        /* this step: non-finite gradients seen (written by apply_update)  */
+  int32_t headroom;    /* S exponent target: max|g| max|w_head| omega S < 2^headroom       */
+  int32_t clean;       /* consecutive clean steps since the last overflow                   */
+  int32_t overflows;   /* steps skipped and recomputed so far                               */
+  int32_t headroom0;   /* initial / maximum headroom                                       */
+  int32_t pad0;
+} siren_guard;
 
 /* ---- one L x H network (SirenWithSnakeTanh, models.py:306-394) ------------------------
  * net.0 = SineLayer(in, H, is_first, omega0); then L inner layers H -> H, each a
@@ -125,6 +144,10 @@ typedef struct siren_batch {
    * of the backward runs.  [i < L]: inner layer i (W_i, b_i, Snake a_i);
    * [L]: the first layer (W0, b0); [L+1]: the head (w_head, b_head) and `sse`. */
   void* grad_ready[SIREN_MAX_INNER + 2];
+  /* run.py:161-169 loss_mode: 0 = MSELoss (sse = sum err^2, g = 2 err / n_total), 1 = L1Loss
+   * ('mae': sse slot = sum |err|, g = sign(err) / n_total) */
+  int32_t loss_mode, pad1;
+  const siren_guard* guard;  /* range guard (NULL: fixed headroom 6, no overflow recovery) */
 } siren_batch;
 
 /* Workspace sizing / tiling helpers.  siren_nt_tile: tile edge the NT GEMMs use for
@@ -154,11 +177,18 @@ int siren_apply_update(const siren_net* net, float* params, const float* grads_f
                        float* const* W_fp32 /* [n_inner] views into params */,
                        uint16_t* const* Wh, uint16_t* const* WTh,
                        siren_opt_state* state, const float* sse, double n_total,
-                       float* loss_hist, double* lr_hist, int64_t hist_cap, void* stream);
+                       float* loss_hist, double* lr_hist, int64_t hist_cap,
+                       siren_guard* guard /* NULL: no range check */, void* stream);
 
 /* ---- individual kernels (parity tests call these one by one) ------------------------ */
 /* utils.py:99-109 get_coord: torch.linspace(-1,1,n_total) at [offset, offset+rows) */
 int siren_coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, void* stream);
+/* utils.py:211-220 MultiWaveformFitting grid, rows [offset, offset+rows) of the height-major
+ * (time, channel) grid: xy[r] = (linspace(-1,1,height)[k / width], ch[k % width]) with
+ * k = offset + r, ch = linspace(-1,1,width) (all 0 when width == 1); rows past
+ * height*width are (0, 0).  Bit-exact with torch.linspace. */
+int siren_coords_fill_grid(float* xy, int64_t rows, int64_t offset, int64_t height, int32_t width,
+                           void* stream);
 /* models.py:114-115 first SineLayer: a0 = omega0*(t W0^T + b0) in fp32, Y0 = sin a0 and
  * C0 = cos a0 (one fp32 sincosf range reduction) -> fp16 */
 int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float* b0, float omega0,
@@ -176,12 +206,13 @@ int siren_inner_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, i
                         uint16_t* C, uint16_t* E, const float* head_w, float* head_part,
                         void* stream);
 /* run.py:125,168 MSELoss + final Linear bias: out, g = 2(out-y)/n_total, partial sums
- * (gmax_part may be NULL) */
+ * (gmax_part may be NULL); the L1Loss of loss_mode 1 is reached through siren_train_step */
 int siren_head_loss(const float* head_part, int32_t nparts, int32_t rows, const float* b_head,
                     const float* y, int32_t n_valid, double n_total, float* out, float* g,
                     float* sse_part, float* gsum_part, float* gmax_part, void* stream);
 /* backward storage scale: gscale = {S, 1/S}, S = 2^k with max|g|*max|w_head|*omega*S < 2^6,
- * from the nparts = rows/256 max |g| partials of siren_head_loss */
+ * from the nparts = rows/256 max |g| partials of siren_head_loss (siren_train_step takes the
+ * exponent from batch->guard->headroom instead of 6) */
 int siren_grad_scale(const float* gmax_part, int32_t nparts, const float* w_head, int32_t hidden,
                      float omega, float* gscale, void* stream);
 /* autograd of Linear(H,1) + the last layer's activation: dZ_L = g w_head omega C (x S),
@@ -219,7 +250,9 @@ int siren_col_reduce(const float* part, int64_t row_stride, int32_t nrows, int32
 /* torch.optim.Adam step over a flat fp32 vector (run.py:186) */
 int siren_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                     const siren_opt_state* state, void* stream);
-/* ReduceLROnPlateau.step(loss) (run.py:187); also increments state->step */
+/* ReduceLROnPlateau.step(loss) (run.py:187); also increments state->step.  The history slot
+ * is state->last_epoch (scheduler steps of this run), not the Adam step: a run resumed from a
+ * checkpoint (run.py:84-106) restores the Adam step but builds a fresh scheduler. */
 int siren_plateau_step(siren_opt_state* state, const float* sse, double n_total, float* loss_hist,
                        double* lr_hist, int64_t hist_cap, void* stream);
 /* fp16 shadows W and W^T of a fp32 [H_out][H_in] weight */

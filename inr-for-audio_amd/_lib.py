@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_INNER = 16
 ROW_TILE = 128
 ACT_SINE, ACT_SNAKE, ACT_TANH = 0, 1, 2  # siren_act
@@ -34,6 +34,15 @@ class SirenOptState(ctypes.Structure):
         ("patience", _i32), ("pad0", _i32),
         ("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
     ]
+
+
+class SirenGuard(ctypes.Structure):
+    """siren_guard: fp16 backward range guard (include/siren_hip.h)."""
+    _fields_ = [("flag", _i32), ("headroom", _i32), ("clean", _i32), ("overflows", _i32),
+                ("headroom0", _i32), ("pad0", _i32)]
+
+
+HEADROOM0 = 6
 
 
 class SirenNet(ctypes.Structure):
@@ -68,6 +77,7 @@ class SirenBatch(ctypes.Structure):
         ("gmax_part", _p), ("gscale", _p), ("col_part", _p), ("col_part2", _p), ("red_tmp", _p), ("slab", _p),
         ("E", _p * (MAX_INNER + 1)),
         ("grad_ready", _p * (MAX_INNER + 2)),
+        ("loss_mode", _i32), ("pad1", _i32), ("guard", _p),
     ]
 
 
@@ -111,8 +121,9 @@ _SIGS = {
                                       ctypes.POINTER(SirenBatch), _p]),
     "siren_apply_update": (ctypes.c_int, [ctypes.POINTER(SirenNet), _p, _p, _p, _p, _i64,
                                           ctypes.POINTER(_p), ctypes.POINTER(_p), ctypes.POINTER(_p),
-                                          _p, _p, ctypes.c_double, _p, _p, _i64, _p]),
+                                          _p, _p, ctypes.c_double, _p, _p, _i64, _p, _p]),
     "siren_coords_fill": (ctypes.c_int, [_p, _i64, _i64, _i64, _p]),
+    "siren_coords_fill_grid": (ctypes.c_int, [_p, _i64, _i64, _i64, _i32, _p]),
     "siren_first_fwd": (ctypes.c_int, [_p, _i32, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p]),
     "siren_inner_fwd": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p]),
     "siren_head_loss": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _i32, ctypes.c_double, _p, _p, _p, _p,
@@ -146,7 +157,7 @@ _SIGS = {
                                           ctypes.POINTER(_i64)]),
 }
 
-STRUCTS = [SirenNet, SirenGrads, SirenBatch, SirenOptState, SirenKanNet, SirenKanGrads, SirenKanBatch]
+STRUCTS = [SirenNet, SirenGrads, SirenBatch, SirenOptState, SirenKanNet, SirenKanGrads, SirenKanBatch, SirenGuard]
 
 PROF_KINDS = ["first_fwd", "inner_fwd", "head", "bwd_dw", "bwd_dx", "bwd_dx0", "reduce", "update"]
 

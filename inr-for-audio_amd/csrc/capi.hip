@@ -8,6 +8,7 @@
 using namespace siren;
 
 static_assert(sizeof(siren_opt_state) == sizeof(OptState), "opt state layout");
+static_assert(sizeof(siren_guard) == sizeof(GuardState), "guard layout");
 
 namespace {
 
@@ -92,6 +93,7 @@ int check_batch(const siren_net* n, const siren_batch* b, bool train) {
       return SIREN_ERR_NULL;
     if (b->splits < 1 || b->n_total <= 0) return SIREN_ERR_CONFIG;
   }
+  if (b->loss_mode < 0 || b->loss_mode > 1) return SIREN_ERR_CONFIG;
   return SIREN_OK;
 }
 
@@ -141,6 +143,7 @@ int64_t siren_struct_size(int32_t which) {
     case 4: return sizeof(siren_kan_net);
     case 5: return sizeof(siren_kan_grads);
     case 6: return sizeof(siren_kan_batch);
+    case 7: return sizeof(siren_guard);
   }
   return -1;
 }
@@ -207,7 +210,8 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
   const bool snake_last = net->act[L - 1] == SIREN_ACT_SNAKE;
   float* da_last = b->col_part + (int64_t)(R / 128) * H;  // second H-wide slab of col_part
   SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale(b->gmax_part, (R + 255) / 256, net->w_head, H,
-                                            act_bound(net, L - 1), b->gscale, s));
+                                            act_bound(net, L - 1), b->gscale, s,
+                                            (const GuardState*)b->guard));
   SIREN_PROF(SIREN_PROF_HEAD, s, head_bwd(B(b->C[L]), B(b->Y[L]), b->g, net->w_head, act_omega(net, L - 1),
                                           R, H, b->gscale, B(b->dZ[0]), b->col_part, b->col_part2,
                                           snake_last ? B(b->E[L]) : nullptr, snake_last ? da_last : nullptr, s));
@@ -284,12 +288,13 @@ int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b
 
   if (b->zero_grads && gr->flat) SIREN_TRY(hipMemsetAsync(gr->flat, 0, gr->flat_len * sizeof(float), s));
 
-  // ---- forward (models.py:388-394) + MSE (run.py:168) ----
+  // ---- forward (models.py:388-394) + MSE / L1 (run.py:161-169) ----
   SIREN_TRY(run_forward(net, b, s));
-  const float gfac = (float)(2.0 / b->n_total);  // MSELoss mean backward: 2/N
+  // mean backward: MSELoss 2 err / N, L1Loss sign(err) / N
+  const float gfac = (float)((b->loss_mode == 1 ? 1.0 : 2.0) / b->n_total);
   SIREN_PROF(SIREN_PROF_HEAD, s, head_loss(b->head_part, H / nt_choose_tile(R, H), R, net->b_head,
                                            b->target, b->n_valid, gfac, b->out, b->g, b->sse_part,
-                                           b->gsum_part, b->gmax_part, s, net->head_omega));
+                                           b->gsum_part, b->gmax_part, s, net->head_omega, b->loss_mode));
   const int nsum = (R + 255) / 256;
   SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->sse_part, nsum, gr->sse, 1, s));
   SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->gsum_part, nsum, gr->b_head, 1, s));
@@ -317,17 +322,21 @@ int siren_backward(const siren_net* net, const siren_grads* gr, siren_batch* b, 
 int siren_apply_update(const siren_net* net, float* params, const float* grads_flat, float* exp_avg,
                        float* exp_avg_sq, int64_t n_params, float* const* W_fp32, uint16_t* const* Wh,
                        uint16_t* const* WTh, siren_opt_state* state, const float* sse, double n_total,
-                       float* loss_hist, double* lr_hist, int64_t hist_cap, void* stream) {
+                       float* loss_hist, double* lr_hist, int64_t hist_cap, siren_guard* guard,
+                       void* stream) {
   int st = check_net(net);
   if (st) return st;
   if (!params || !grads_flat || !exp_avg || !exp_avg_sq || !state || !sse || !W_fp32 || !Wh || !WTh)
     return SIREN_ERR_NULL;
   hipStream_t s = S(stream);
+  GuardState* gd = (GuardState*)guard;
+  if (gd) SIREN_PROF(SIREN_PROF_UPDATE, s, guard_check(grads_flat, n_params, gd, s));
   SIREN_PROF(SIREN_PROF_UPDATE, s, adam_flat(params, grads_flat, exp_avg, exp_avg_sq, n_params,
-                                             (const OptState*)state, s));
+                                             (const OptState*)state, s, gd, sse));
   for (int i = 0; i < net->n_inner; ++i)
     SIREN_PROF(SIREN_PROF_UPDATE, s, cast_weight(W_fp32[i], net->hidden, net->hidden, B(Wh[i]), B(WTh[i]), s));
-  SIREN_PROF(SIREN_PROF_UPDATE, s, plateau_step((OptState*)state, sse, n_total, loss_hist, lr_hist, hist_cap, s));
+  SIREN_PROF(SIREN_PROF_UPDATE, s, plateau_step((OptState*)state, sse, n_total, loss_hist, lr_hist, hist_cap, s,
+                                                gd));
   return SIREN_OK;
 }
 
@@ -337,6 +346,13 @@ int siren_coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, v
   if (!t) return SIREN_ERR_NULL;
   if (rows < 0 || offset < 0 || n_total < 1) return SIREN_ERR_SHAPE;
   return (int)coords_fill(t, rows, offset, n_total, S(stream));
+}
+
+int siren_coords_fill_grid(float* xy, int64_t rows, int64_t offset, int64_t height, int32_t width,
+                           void* stream) {
+  if (!xy) return SIREN_ERR_NULL;
+  if (rows < 0 || offset < 0 || height < 1 || width < 1) return SIREN_ERR_SHAPE;
+  return (int)coords_fill_grid(xy, rows, offset, height, width, S(stream));
 }
 
 int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float* b0, float omega0,

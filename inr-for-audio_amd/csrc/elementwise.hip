@@ -38,6 +38,38 @@ hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, 
   return hipGetLastError();
 }
 
+// torch.linspace(-1, 1, n)[i] in fp32 (the same contracted form as coords_fill_kernel)
+__device__ __forceinline__ float linspace_at(int64_t i, int64_t n) {
+  if (n == 1) return -1.0f;
+  const float step = 2.0f / (float)(n - 1);
+  return (i < n / 2) ? __builtin_fmaf(step, (float)i, -1.0f) : __builtin_fmaf(-step, (float)(n - 1 - i), 1.0f);
+}
+
+// MultiWaveformFitting's (time, channel) grid (utils.py:211-220): row k of the height-major
+// meshgrid is (linspace(-1,1,height)[k / width], linspace(-1,1,width)[k % width]), channel 0
+// when width == 1 (linspace(0, 0, 1)).  One float2 per row, coalesced 8-B stores.
+__global__ void coords_grid_kernel(float2* xy, int64_t rows, int64_t offset, int64_t height, int width) {
+  const int64_t n = height * width;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = offset + r;
+    float2 v = {0.f, 0.f};
+    if (k < n) {
+      const int64_t i = k / width;
+      const int j = (int)(k - i * width);
+      v.x = linspace_at(i, height);
+      v.y = width == 1 ? 0.f : linspace_at(j, width);
+    }
+    xy[r] = v;
+  }
+}
+
+hipError_t coords_fill_grid(float* xy, int64_t rows, int64_t offset, int64_t height, int width, hipStream_t s) {
+  hipLaunchKernelGGL(coords_grid_kernel, dim3(grid_for(rows, 256)), dim3(256), 0, s, (float2*)xy, rows, offset,
+                     height, width);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------
 // First SineLayer (is_first=True, models.py:105-115): y0 = sin(omega0 * (t W0^T + b0)).
 // Kept in fp32 end to end: |omega0*z| reaches ~4.4e4 rad at omega0 = 22000, so the
@@ -129,13 +161,15 @@ hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b
 // Final nn.Linear(H,1) + MSELoss (models.py:374-381, run.py:125,168):
 //   out = sum_j head_part[j][m] + b;  err = out - y;  g = err * (2/N_total) (0 on pad rows)
 // plus per-block partial sums of err^2 (loss) and g (bias gradient), and per-block max |g|
-// (for grad_scale).
+// (for grad_scale).  loss_mode 1 = L1Loss (run.py:124, 161-163, loss_mode='mae'): the loss
+// term is |err| and g = sign(err) * (1/N_total) (torch's sign: 0 at err == 0); the caller
+// passes gfac = 1/N_total then.
 __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts, int R,
                                  const float* __restrict__ b_head, const float* __restrict__ y,
                                  int n_valid, float gfac, float* __restrict__ out,
                                  float* __restrict__ g, float* __restrict__ sse_part,
                                  float* __restrict__ gsum_part, float* __restrict__ gmax_part,
-                                 float head_omega) {
+                                 float head_omega, int loss_mode) {
   __shared__ float scratch[4];
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   float e2 = 0.f, gv = 0.f;
@@ -150,8 +184,13 @@ __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts
     out[m] = ov;
     if (m < n_valid) {
       const float err = ov - y[m];
-      e2 = err * err;
-      gv = err * gfac;
+      if (loss_mode == 1) {
+        e2 = fabsf(err);
+        gv = (err > 0.f ? 1.0f : (err < 0.f ? -1.0f : 0.f)) * gfac;
+      } else {
+        e2 = err * err;
+        gv = err * gfac;
+      }
       if (head_omega > 0.f) gv = (gv * cosf(a)) * head_omega;
     }
     g[m] = gv;
@@ -168,9 +207,9 @@ __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts
 
 hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_head, const float* y,
                      int n_valid, float gfac, float* out, float* g, float* sse_part,
-                     float* gsum_part, float* gmax_part, hipStream_t s, float head_omega) {
+                     float* gsum_part, float* gmax_part, hipStream_t s, float head_omega, int loss_mode) {
   hipLaunchKernelGGL(head_loss_kernel, dim3((R + 255) / 256), dim3(256), 0, s, head_part, nparts, R,
-                     b_head, y, n_valid, gfac, out, g, sse_part, gsum_part, gmax_part, head_omega);
+                     b_head, y, n_valid, gfac, out, g, sse_part, gsum_part, gmax_part, head_omega, loss_mode);
   return hipGetLastError();
 }
 
@@ -213,10 +252,11 @@ hipError_t gmax_partials(const float* g, int R, float* gmax_part, hipStream_t s)
 // stores dZ * S with S = 2^k chosen so that its bound max|g| * max|w_head| * omega lands
 // just under 2^6 (headroom for growth through the layers below), and every fp32 gradient
 // reduced from a scaled dZ is multiplied by 1/S.  Powers of two: scaling is exact.
-// gscale[0] = S, gscale[1] = 1/S.  One block.
+// gscale[0] = S, gscale[1] = 1/S.  One block.  The exponent target (6 above) comes from the
+// range guard when one is given: siren_apply_update lowers it after an fp16 overflow.
 __global__ void grad_scale_kernel(const float* __restrict__ gmax_part, int nparts,
                                   const float* __restrict__ w_head, int H, float omega,
-                                  float* __restrict__ gscale) {
+                                  float* __restrict__ gscale, const GuardState* __restrict__ guard) {
   __shared__ float scratch[4];
   float gm = 0.f, wm = 0.f;
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) gm = fmaxf(gm, gmax_part[i]);
@@ -229,7 +269,7 @@ __global__ void grad_scale_kernel(const float* __restrict__ gmax_part, int npart
     if (bound > 0.f && bound < INFINITY) {
       int e;
       (void)frexpf(bound, &e);  // bound < 2^e
-      k = 6 - e;
+      k = (guard ? guard->headroom : kHeadroomDefault) - e;
       k = k < -100 ? -100 : (k > 100 ? 100 : k);
     }
     gscale[0] = ldexpf(1.0f, k);
@@ -238,9 +278,9 @@ __global__ void grad_scale_kernel(const float* __restrict__ gmax_part, int npart
 }
 
 hipError_t grad_scale(const float* gmax_part, int nparts, const float* w_head, int H, float omega,
-                      float* gscale, hipStream_t s) {
+                      float* gscale, hipStream_t s, const GuardState* guard) {
   hipLaunchKernelGGL(grad_scale_kernel, dim3(1), dim3(256), 0, s, gmax_part, nparts, w_head, H, omega,
-                     gscale);
+                     gscale, guard);
   return hipGetLastError();
 }
 
@@ -385,11 +425,14 @@ hipError_t sum_to(const float* x, int n, float* out, int accumulate, hipStream_t
 //   v = fma((1-b2)*g, g, v*b2)                 (mul_ + addcmul_)
 //   d = sqrt(v) / sqrt(bc2) + eps              (correctly rounded sqrt/div)
 //   p = p + ((-lr/bc1) * m) / d                (addcdiv_)
-// bias corrections in fp64 from the device step counter.
+// bias corrections in fp64 from the device step counter.  A step the range guard rejects
+// (guard_skip) leaves p, m, v untouched.
 __global__ void adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
                                  float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                 const OptState* __restrict__ st) {
+                                 const OptState* __restrict__ st, const GuardState* __restrict__ guard,
+                                 const float* __restrict__ sse) {
 #pragma clang fp contract(off)
+  if (guard_skip(guard, sse)) return;
   const double step = st->step + 1.0;
   const double bc1 = 1.0 - pow(st->beta1, step);
   const double bc2 = 1.0 - pow(st->beta2, step);
@@ -414,22 +457,57 @@ __global__ void adam_flat_kernel(float* __restrict__ p, const float* __restrict_
 }
 
 hipError_t adam_flat(float* p, const float* g, float* m, float* v, int64_t n, const OptState* st,
-                     hipStream_t s) {
+                     hipStream_t s, const GuardState* guard, const float* sse) {
   hipLaunchKernelGGL(adam_flat_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0, s, p, g, m, v, n,
-                     st);
+                     st, guard, sse);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// Range guard check (siren_apply_update, before Adam): guard->flag |= any non-finite value
+// in the reduced gradient vector g[0..n).  One atomic per block that found one.
+__global__ void guard_check_kernel(const float* __restrict__ g, int64_t n, GuardState* guard) {
+  __shared__ float scratch[4];
+  float bad = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (!__builtin_isfinite(g[i])) bad = 1.f;
+  bad = block_max(bad, scratch);
+  if (threadIdx.x == 0 && bad > 0.f) atomicOr(&guard->flag, 1);
+}
+
+hipError_t guard_check(const float* g, int64_t n, GuardState* guard, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(&guard->flag, 0, sizeof(int32_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(guard_check_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, s, g, n, guard);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
 // ReduceLROnPlateau(mode='min', factor, patience, threshold=1e-4 rel, min_lr, eps=1e-8)
 // .step(loss) (run.py:117,187) on device, after Adam used the current lr.  Also bumps the
-// Adam step counter and records (loss, lr) history for the host to fetch lazily.
+// Adam step counter and records (loss, lr) history for the host to fetch lazily, at index
+// last_epoch = scheduler steps of THIS run (a resumed run restores the Adam step from the
+// checkpoint but, like run.py:106, starts a fresh scheduler).  A step the range guard
+// rejects advances nothing: it lowers the guard's headroom instead, and the caller's next
+// step recomputes the same gradients with the smaller backward scale.
 __global__ void plateau_kernel(OptState* st, const float* sse, double n_total, float* loss_hist,
-                               double* lr_hist, int64_t hist_cap) {
+                               double* lr_hist, int64_t hist_cap, GuardState* guard) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (guard) {
+    if (guard_skip(guard, sse)) {
+      guard->headroom -= kHeadroomDrop;
+      guard->clean = 0;
+      guard->overflows += 1;
+      return;
+    }
+    if (++guard->clean >= kHeadroomGrowAfter) {
+      guard->clean = 0;
+      if (guard->headroom < guard->headroom0) guard->headroom += 1;
+    }
+  }
   const float loss = (float)((double)sse[0] / n_total);
   const double cur = (double)loss;
-  const int64_t k = (int64_t)st->step;  // index of this optimizer step (0-based)
+  const int64_t k = (int64_t)st->last_epoch;  // index of this scheduler step in this run (0-based)
   st->step = st->step + 1.0;
   st->last_epoch += 1;
   if (cur < st->best * (1.0 - st->threshold)) {
@@ -451,9 +529,9 @@ __global__ void plateau_kernel(OptState* st, const float* sse, double n_total, f
 }
 
 hipError_t plateau_step(OptState* st, const float* sse, double n_total, float* loss_hist,
-                        double* lr_hist, int64_t hist_cap, hipStream_t s) {
+                        double* lr_hist, int64_t hist_cap, hipStream_t s, GuardState* guard) {
   hipLaunchKernelGGL(plateau_kernel, dim3(1), dim3(64), 0, s, st, sse, n_total, loss_hist, lr_hist,
-                     hist_cap);
+                     hist_cap, guard);
   return hipGetLastError();
 }
 

@@ -75,19 +75,36 @@ hipError_t dw_reduce(const float* slab, int splits, int Hin, int Hout, int tile,
 
 // elementwise / reduction kernels (elementwise.hip)
 hipError_t coords_fill(float* t, int64_t rows, int64_t offset, int64_t n_total, hipStream_t s);
+hipError_t coords_fill_grid(float* xy, int64_t rows, int64_t offset, int64_t height, int width, hipStream_t s);
+
+// fp16 backward range guard (include/siren_hip.h siren_guard)
+struct GuardState {
+  int32_t flag, headroom, clean, overflows, headroom0, pad0;
+};
+constexpr int kHeadroomDefault = 6;      // grad_scale target exponent without a guard
+constexpr int kHeadroomDrop = 4;         // per rejected step (S / 16)
+constexpr int kHeadroomMin = -14;        // below this a non-finite gradient is passed through
+constexpr int kHeadroomGrowAfter = 1000; // clean steps before headroom grows back by one
+// true when the step's gradients hold a non-finite value, the loss is finite (so it is the
+// fp16 dZ storage that overflowed, not a diverged fit) and the headroom can still drop
+__device__ __forceinline__ bool guard_skip(const GuardState* g, const float* sse) {
+  return g && g->flag && __builtin_isfinite(sse[0]) && g->headroom > kHeadroomMin;
+}
+hipError_t guard_check(const float* g, int64_t n, GuardState* guard, hipStream_t s);
 // a0 / E0 non-null: Linear + Snake first layer (first_linear=True); C0 null: Y0 only
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
                      int R, int H, h16* Y0, h16* C0, hipStream_t s, const float* a0 = nullptr,
                      h16* E0 = nullptr);
 hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_head, const float* y,
                      int n_valid, float gfac, float* out, float* g, float* sse_part,
-                     float* gsum_part, float* gmax_part, hipStream_t s, float head_omega = 0.f);
+                     float* gsum_part, float* gmax_part, hipStream_t s, float head_omega = 0.f,
+                     int loss_mode = 0);
 hipError_t gmax_partials(const float* g, int R, float* gmax_part, hipStream_t s);
 hipError_t head_sine_chain(const float* head_part, int nparts, int R, const float* b_head, float omega, float* g,
                            hipStream_t s);
 // gscale[0] = S (dZ storage scale), gscale[1] = 1/S; from (R+255)/256 max|g| partials
 hipError_t grad_scale(const float* gmax_part, int nparts, const float* w_head, int H, float omega,
-                      float* gscale, hipStream_t s);
+                      float* gscale, hipStream_t s, const GuardState* guard = nullptr);
 // E != null (Snake last layer): da_part[R/128][H] = partial sums of g*w_head*E
 hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_head, float omega,
                     int R, int H, const float* gscale, h16* dZ, float* db_part, float* dwh_part,
@@ -119,9 +136,9 @@ struct OptState {      // device-resident optimizer + ReduceLROnPlateau state (r
 };
 
 hipError_t adam_flat(float* p, const float* g, float* m, float* v, int64_t n, const OptState* st,
-                     hipStream_t s);
+                     hipStream_t s, const GuardState* guard = nullptr, const float* sse = nullptr);
 hipError_t plateau_step(OptState* st, const float* sse, double n_total, float* loss_hist,
-                        double* lr_hist, int64_t hist_cap, hipStream_t s);
+                        double* lr_hist, int64_t hist_cap, hipStream_t s, GuardState* guard = nullptr);
 hipError_t cast_weight(const float* W, int H_out, int H_in, h16* Wb, h16* WTb, hipStream_t s);
 hipError_t sum_to(const float* x, int n, float* out, int accumulate, hipStream_t s);
 

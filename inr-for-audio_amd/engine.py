@@ -83,7 +83,12 @@ class ParamLayout:
 
 
 class Workspace:
-    """Activations + scratch for `rows` coordinates (rows % 128 == 0)."""
+    """Activations + scratch for `rows` coordinates (rows % 128 == 0).
+
+    Training keeps every layer's Y / C (and Snake E) for the backward.  Inference
+    (train=False) needs only the layer input and output at a time: Y ping-pongs between two
+    buffers and every C / E points at one write-only scratch buffer, so an inference
+    workspace is 3-4 activation buffers whatever the depth."""
 
     def __init__(self, spec: NetSpec, rows: int, device, train: bool = True, splits: int | None = None):
         lib = _lib.load()
@@ -93,11 +98,21 @@ class Workspace:
         h, f32 = STORE16, torch.float32
         e = lambda *s, dtype=f32: torch.empty(*s, dtype=dtype, device=device)  # noqa: E731
         self.rows = R
-        self.Y = [e(R, H, dtype=h) for _ in range(L + 1)]
-        self.C = [e(R, H, dtype=h) for _ in range(L + 1)]
-        # dY/da of Snake layers (E[i+1] for inner layer i)
-        self.E = [e(R, H, dtype=h) if spec.first_snake else None] + \
-            [e(R, H, dtype=h) if spec.act(i) == _lib.ACT_SNAKE else None for i in range(L)]
+        if train:
+            self.Y = [e(R, H, dtype=h) for _ in range(L + 1)]
+            self.C = [e(R, H, dtype=h) for _ in range(L + 1)]
+            # dY/da of Snake layers (E[i+1] for inner layer i)
+            self.E = [e(R, H, dtype=h) if spec.first_snake else None] + \
+                [e(R, H, dtype=h) if spec.act(i) == _lib.ACT_SNAKE else None for i in range(L)]
+        else:
+            ping = [e(R, H, dtype=h), e(R, H, dtype=h)]
+            scratch = e(R, H, dtype=h)
+            self.Y = [ping[i % 2] for i in range(L + 1)]
+            self.C = [scratch] * (L + 1)
+            snake = spec.first_snake or any(spec.act(i) == _lib.ACT_SNAKE for i in range(L))
+            escr = e(R, H, dtype=h) if snake else None
+            self.E = [escr if spec.first_snake else None] + \
+                [escr if spec.act(i) == _lib.ACT_SNAKE else None for i in range(L)]
         self.out = e(R)
         self.g = torch.zeros(R, dtype=f32, device=device)
         self.head_part = e(H // 128, R)
@@ -120,10 +135,11 @@ class Workspace:
             self.col_part = self.col_part2 = self.red_tmp = self.slab = None
 
     def batch(self, coords: torch.Tensor, target, n_valid: int, n_total: float,
-              zero_grads: bool = False) -> SirenBatch:
+              zero_grads: bool = False, guard: torch.Tensor | None = None, loss_mode: int = 0) -> SirenBatch:
         b = SirenBatch()
         b.rows, b.n_valid, b.n_total = self.rows, int(n_valid), float(n_total)
         b.splits, b.zero_grads = self.splits, int(zero_grads)
+        b.guard, b.loss_mode = ptr(guard), int(loss_mode)
         b.coords, b.target = ptr(coords), ptr(target)
         for i, y in enumerate(self.Y):
             b.Y[i] = ptr(y)
@@ -182,6 +198,16 @@ def cast_shadows(spec, Ws, Whs, WThs, stream):
               "siren_cast_weight")
 
 
+LOSS_MODES = {"mse": 0, "mae": 1}   # run.py:161-169 (MSELoss / L1Loss)
+
+
+def new_guard(device) -> torch.Tensor:
+    """A zeroed siren_guard with the default headroom (include/siren_hip.h)."""
+    g = torch.zeros(6, dtype=torch.int32)
+    g[1] = g[4] = _lib.HEADROOM0
+    return g.to(device)
+
+
 def _dist():
     d = torch.distributed
     if d.is_available() and d.is_initialized() and d.get_world_size() > 1:
@@ -206,9 +232,11 @@ class SirenEngine:
     def __init__(self, model, coords: torch.Tensor, target: torch.Tensor, *, lr: float = 1e-3,
                  min_lr: float = 1e-6, factor: float = 0.8, patience: int = 200,
                  n_total: int | None = None, micro_batch: int = 1 << 20, hist_cap: int = 20000,
-                 splits: int | None = None, device=None):
+                 splits: int | None = None, device=None, loss_mode: str = "mse"):
         lib = _lib.load()
         self.lib = lib
+        if loss_mode not in LOSS_MODES:
+            raise NotImplementedError(f"loss_mode={loss_mode!r}: the HIP path has {sorted(LOSS_MODES)}")
         self.device = torch.device(device or "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("SirenEngine runs on the GPU only (HIP kernels; no CPU fallback)")
@@ -278,12 +306,14 @@ class SirenEngine:
         self.coords[:n] = coords.to(dev)
         self.target[:n] = target.to(dev)
         self.ws = Workspace(spec, mb, dev, train=True, splits=splits)
+        self.guard = new_guard(dev)
         self.batches = []
         for k in range(self.n_micro):
             lo = k * mb
             c = self.coords[lo:lo + mb]
             t = self.target[lo:lo + mb]
-            self.batches.append(self.ws.batch(c, t, min(mb, n - lo), n_global, zero_grads=(k == 0)))
+            self.batches.append(self.ws.batch(c, t, min(mb, n - lo), n_global, zero_grads=(k == 0),
+                                              guard=self.guard, loss_mode=LOSS_MODES[loss_mode]))
         self.steps_done = 0
         self.graph = None
         if d is not None:
@@ -329,7 +359,7 @@ class SirenEngine:
             ctypes.byref(self.net), ptr(self.params), ptr(self.grads), ptr(self.exp_avg),
             ptr(self.exp_avg_sq), self.layout.n_params, self._Wp, self._Whp, self._WThp,
             ptr(self.state), self.grads.data_ptr() + 4 * self.layout.sse_offset, float(self.n_total),
-            ptr(self.loss_hist), ptr(self.lr_hist), self.hist_cap, self._stream()),
+            ptr(self.loss_hist), ptr(self.lr_hist), self.hist_cap, ptr(self.guard), self._stream()),
             "siren_apply_update")
 
     # ------------------------------------------------------------------ public API
@@ -376,13 +406,34 @@ class SirenEngine:
     def opt_state(self) -> SirenOptState:
         return SirenOptState.from_buffer_copy(bytes(self.state.cpu().numpy().tobytes()))
 
+    def steps_applied(self) -> int:
+        """Optimizer steps taken by this engine (scheduler steps of this run); step() calls
+        minus the ones the fp16 range guard rejected and recomputed (synchronises)."""
+        return int(self.opt_state().last_epoch)
+
+    def guard_state(self) -> dict:
+        """{'headroom', 'overflows', 'clean'} of the fp16 backward range guard (synchronises)."""
+        if getattr(self, "guard", None) is None:
+            return {"headroom": None, "overflows": 0, "clean": 0}
+        g = self.guard.cpu().tolist()
+        return {"headroom": g[1], "overflows": g[3], "clean": g[2]}
+
+    def run(self, steps: int) -> None:
+        """`steps` optimizer steps: step() calls, plus one more for each step the fp16 range
+        guard rejected (checked once at the end -- no per-step host synchronisation)."""
+        start = self.steps_applied()
+        for _ in range(steps):
+            self.step()
+        while self.steps_applied() - start < steps:
+            self.step()
+
     def history(self):
-        """(losses, lrs) of the steps done so far (host copies)."""
-        k = min(self.steps_done, self.hist_cap)
+        """(losses, lrs) of the optimizer steps applied so far (host copies)."""
+        k = min(self.steps_applied(), self.hist_cap)
         return self.loss_hist[:k].cpu().numpy(), self.lr_hist[:k].cpu().numpy()
 
     def last_loss(self) -> float:
-        k = min(self.steps_done, self.hist_cap) - 1
+        k = min(self.steps_applied(), self.hist_cap) - 1
         return float(self.loss_hist[k].item()) if k >= 0 else float("nan")
 
     def grad_views(self):
@@ -390,9 +441,13 @@ class SirenEngine:
 
     @torch.no_grad()
     def infer(self, coords: torch.Tensor, chunk: int | None = None) -> torch.Tensor:
-        """model(coords) with the current weights (run.py:249-256); returns [N] fp32."""
+        """model(coords) with the current weights (run.py:249-256); returns [N] fp32.  Runs
+        in the training workspace (the next step recomputes every activation), so inference
+        allocates nothing beyond the output."""
+        chunk = chunk or self.rows
+        ws = self.ws if round_up(chunk, ROW_TILE) == self.rows else None
         return forward_net(self.spec, self.net, coords.reshape(-1, self.spec.in_dim), self.device,
-                           chunk or self.rows, shadows_ready=True)
+                           chunk, shadows_ready=True, ws=ws)
 
     def adam_state_dict(self):
         """torch.optim.Adam-compatible state_dict (run.py:359-362 checkpoint format)."""
@@ -428,12 +483,16 @@ class SirenEngine:
 
 
 def forward_net(spec: NetSpec, net: SirenNet, coords: torch.Tensor, device, chunk: int,
-                shadows_ready: bool = True) -> torch.Tensor:
-    """Inference through siren_forward in chunks of `chunk` rows."""
+                shadows_ready: bool = True, ws: Workspace | None = None) -> torch.Tensor:
+    """Inference through siren_forward in chunks of `chunk` rows (in `ws` when given, else
+    in a ping-pong inference workspace)."""
     lib = _lib.load()
     n = coords.shape[0]
-    chunk = min(round_up(chunk, ROW_TILE), round_up(max(n, 1), ROW_TILE))
-    ws = Workspace(spec, chunk, device, train=False)
+    if ws is not None:
+        chunk = ws.rows
+    else:
+        chunk = min(round_up(chunk, ROW_TILE), round_up(max(n, 1), ROW_TILE))
+        ws = Workspace(spec, chunk, device, train=False)
     out = torch.empty(n, dtype=torch.float32, device=device)
     buf = torch.zeros(chunk, spec.in_dim, dtype=torch.float32, device=device)
     s = torch.cuda.current_stream(device).cuda_stream

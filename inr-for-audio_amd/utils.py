@@ -73,6 +73,54 @@ class WaveformFitting:
         return self.coord, self.amplitude()
 
 
+class MultiWaveformFitting:
+    """Multi-channel (t, ch) -> amplitude dataset -- utils.py:186-231 (BASELINE cfg3).
+
+    The clip is cast to float32 and trimmed to `duration` seconds and `num_channels` channels
+    (the reference indexes ``data[:T, :num_channels]``, so the file must be multi-channel);
+    with ``lp`` each channel is FIR-decimated by 2 (zero phase), which leaves float64 samples
+    exactly as the reference's ``np.column_stack`` does.  No peak normalisation (the
+    reference's ``__getitem__`` has it commented out).  Coordinates are the height-major
+    (time, channel) grid: time = linspace(-1, 1, height), channel = linspace(-1, 1, width)
+    (all 0 for one channel), flattened row k = (t[k // width], ch[k % width]) -- so the
+    channels of one instant are adjacent rows, and ``samples`` is ``data.reshape(-1, 1)``."""
+
+    def __init__(self, filename=None, duration=1, num_channels=2, lp=False, *, data=None, sample_rate=None):
+        if data is None:
+            self.sample_rate, self.data = wavfile.read(filename)
+        else:
+            self.sample_rate, self.data = int(sample_rate), np.asarray(data)
+        self.data = self.data.astype(np.float32)[: duration * self.sample_rate, :num_channels]
+        self.original_sample_rate = self.sample_rate
+        if lp:
+            q = 2
+            chans = [decimate(self.data[:, i], q, ftype="fir", zero_phase=True) for i in range(num_channels)]
+            self.data = np.column_stack(chans)
+            self.sample_rate = self.sample_rate // q
+        self.height, self.width = self.data.shape
+        height_norm = torch.linspace(-1, 1, steps=self.height)
+        if num_channels == 1:
+            width_norm = torch.linspace(0, 0, steps=self.width)
+        else:
+            width_norm = torch.linspace(-1, 1, steps=self.width)
+        h_grid, w_grid = torch.meshgrid(height_norm, width_norm, indexing="ij")
+        self.coords = torch.stack((h_grid, w_grid), dim=-1).reshape(self.height * self.width, -1)
+        self.samples = self.data.reshape(-1, 1)
+
+    def get_num_samples(self):
+        return self.coords.shape[0]
+
+    def __len__(self):
+        return 1
+
+    def __getitem__(self, idx):
+        return self.coords, self.samples
+
+    def to_channels(self, model_output) -> np.ndarray:
+        """Flat model output in the grid's row order -> [height][width] (time, channel)."""
+        return np.asarray(model_output, dtype=np.float32).reshape(self.height, self.width)
+
+
 def load_mono_like_librosa(filename):
     """librosa.load(filename, sr=None) for WAV: float32, integer PCM scaled to [-1,1),
     multi-channel averaged to mono (run.py:302-303)."""

@@ -9,7 +9,8 @@ A numpy restatement of the reference algorithm (senyuanfan/inr-for-audio):
   * WaveformFitting target normalisation      utils.py:111-149
   * SineLayer / SirenWithSnakeTanh forward    models.py:114-115, 388-394
   * Linear + Snake / Linear + Tanh layers       models.py:235-241, 356-372
-  * MSELoss + autograd backward               run.py:125,168,185
+  * MSELoss / L1Loss + autograd backward       run.py:124-125,161-168,185
+  * MultiWaveformFitting (t, ch) grid           utils.py:186-231
   * torch.optim.Adam step                     run.py:116,186
   * ReduceLROnPlateau(min, 0.8, 200)          run.py:117,187
   * calculate_snr + run.py's reported SNR     utils.py:77-97, run.py:302-335
@@ -52,15 +53,16 @@ def f16_round(x: np.ndarray) -> np.ndarray:
     return np.asarray(x, F32).astype(np.float16).astype(F32)
 
 
-def grad_scale(g: np.ndarray, wf: np.ndarray, omega: float) -> float:
-    """elementwise.hip grad_scale_kernel: S = 2^(6-e) with max|g|*max|w_head|*|omega| in
-    [2^(e-1), 2^e) (fp32 product), k clamped to [-100, 100]; S = 1 if the bound is 0."""
+def grad_scale(g: np.ndarray, wf: np.ndarray, omega: float, headroom: int = 6) -> float:
+    """elementwise.hip grad_scale_kernel: S = 2^(headroom-e) with max|g|*max|w_head|*|omega| in
+    [2^(e-1), 2^e) (fp32 product), k clamped to [-100, 100]; S = 1 if the bound is 0.
+    `headroom` is 6 unless the fp16 range guard lowered it (siren_guard)."""
     bound = F32(F32(np.max(np.abs(np.asarray(g, F32)))) * F32(np.max(np.abs(np.asarray(wf, F32)))))
     bound = F32(bound * F32(abs(omega)))
     if not (bound > 0 and np.isfinite(bound)):
         return 1.0
     _, e = math.frexp(float(bound))
-    return math.ldexp(1.0, int(min(max(6 - e, -100), 100)))
+    return math.ldexp(1.0, int(min(max(headroom - e, -100), 100)))
 
 
 def fma32(a, b, c) -> np.ndarray:
@@ -251,10 +253,11 @@ def mse(out: np.ndarray, y: np.ndarray) -> float:
 
 
 def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float, omega: float,
-             half: bool = False, dtype=F64) -> dict:
+             half: bool = False, dtype=F64, headroom: int = 6) -> dict:
     """Autograd of the SIREN for upstream dLoss/dout = g [N].  Returns a dict of grads in
     nn.Linear layout (same keys as Params.to_state_dict).  With `half`, every dZ_i is
-    rounded as the HIP path stores it: fp16(dZ_i * S) / S (exact power-of-two scale)."""
+    rounded as the HIP path stores it: fp16(dZ_i * S) / S (exact power-of-two scale, S from
+    grad_scale with the given `headroom`)."""
     L = len(p.W)
     Y, A, C, E = cache["Y"], cache["A"], cache["C"], cache.get("E", [None] * (L + 1))
     layers, (hw, hb) = p.keys()
@@ -263,7 +266,7 @@ def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float
         g = (np.asarray(g, F64) * np.cos(p.head_omega * o) * p.head_omega).astype(F32)
     # backward scale bound: |dY/dz| of the last layer (elementwise.hip grad_scale / capi act_bound)
     bound = {"sine": omega, "snake": 2.0, "tanh": 1.0}[p.kinds[-1]]
-    S = grad_scale(g, p.wf, bound) if half else 1.0
+    S = grad_scale(g, p.wf, bound, headroom) if half else 1.0
     g = np.asarray(g, dtype).reshape(-1)
     grads = {}
     grads[hw] = (g @ np.asarray(Y[L], dtype)).reshape(1, -1)
@@ -302,6 +305,27 @@ def mse_grad(out: np.ndarray, y: np.ndarray, n_total: int | None = None) -> np.n
     """MSELoss(mean) backward: (out - y) * (2/N) in fp32 (torch's norm scalar)."""
     n = out.shape[0] if n_total is None else n_total
     return ((np.asarray(out, F32) - np.asarray(y, F32).reshape(-1)) * F32(2.0 / n)).astype(F32)
+
+
+def l1_grad(out: np.ndarray, y: np.ndarray, n_total: int | None = None) -> np.ndarray:
+    """L1Loss(mean) backward (run.py:124, 161-163 loss_mode='mae'): sign(out - y) / N in fp32
+    (torch's sign: 0 where out == y)."""
+    n = out.shape[0] if n_total is None else n_total
+    d = np.asarray(out, F32) - np.asarray(y, F32).reshape(-1)
+    return (np.sign(d).astype(F32) * F32(1.0 / n)).astype(F32)
+
+
+def l1(out: np.ndarray, y: np.ndarray) -> float:
+    return float(np.mean(np.abs(np.asarray(out, F64) - np.asarray(y, F64).reshape(-1))))
+
+
+def multiwave_grid(height: int, width: int) -> np.ndarray:
+    """MultiWaveformFitting's (time, channel) grid (utils.py:211-220): row k =
+    (linspace(-1,1,height)[k // width], ch[k % width]), ch = linspace(-1,1,width), or 0 for
+    one channel.  [height*width][2] fp32."""
+    t = linspace_f32(height)
+    ch = np.zeros(1, F32) if width == 1 else linspace_f32(width)
+    return np.stack([np.repeat(t, width), np.tile(ch, height)], axis=1).astype(F32)
 
 
 # ------------------------------------------------------------------ optimizer (run.py)

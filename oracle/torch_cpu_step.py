@@ -41,14 +41,17 @@ def build(in_dim, hidden, n_inner, omega0, omega, seed=0):
     return nn.Sequential(*layers)
 
 
-def time_steps(n_coords=65536, hidden=1024, n_inner=4, steps=4, threads=None, omega0=3000.0,
-               omega=30.0, seed=0):
+def time_steps(n_coords=65536, hidden=1024, n_inner=4, steps=6, threads=None, omega0=3000.0,
+               omega=30.0, seed=0, in_dim=1):
     """Median wall time of steps 2..k of the full-batch loop (BASELINE.md CPU plan)."""
     if threads:
         torch.set_num_threads(int(threads))
-    model = build(1, hidden, n_inner, omega0, omega, seed)
+    model = build(in_dim, hidden, n_inner, omega0, omega, seed)
     t = torch.linspace(-1, 1, n_coords).reshape(1, n_coords, 1)
     y = 0.5 * torch.sin(37 * t) + 0.3 * torch.sin(91 * t + 0.5)
+    if in_dim == 2:  # (t, ch) rows: channel -1 / +1 alternating
+        ch = torch.where(torch.arange(n_coords) % 2 == 0, -1.0, 1.0).reshape(1, n_coords, 1)
+        t = torch.cat([t, ch], -1)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.8, patience=200,
                                                        min_lr=1e-6)
@@ -66,4 +69,4 @@ def time_steps(n_coords=65536, hidden=1024, n_inner=4, steps=4, threads=None, om
         times.append(time.perf_counter() - t0)
     med = float(np.median(times[1:])) if len(times) > 1 else times[0]
     return {"sec_per_step": med, "coord_samples_per_sec": n_coords / med,
-            "threads": torch.get_num_threads(), "n_coords": n_coords, "steps": steps}
+            "threads": torch.get_num_threads(), "n_coords": n_coords, "steps": steps, "step_times": times}

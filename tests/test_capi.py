@@ -44,7 +44,7 @@ def test_struct_layouts_match(lib):
 
 
 def test_host_only_helpers(lib):
-    assert lib.siren_abi_version() == 4
+    assert lib.siren_abi_version() == 5
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256
@@ -71,6 +71,12 @@ def test_validation_without_device(lib):
     assert lib.siren_grad_scale(None, 1, 1, 256, ctypes.c_float(30), 1, None) == 1002
     assert lib.siren_grad_scale(1, 0, 1, 256, ctypes.c_float(30), 1, None) == 1001
     assert lib.siren_first_fwd(1, 3, 1, 1, ctypes.c_float(1.0), 128, 256, 1, 1, None) == 1003
+    assert lib.siren_coords_fill_grid(None, 8, 0, 4, 2, None) == 1002
+    assert lib.siren_coords_fill_grid(1, 8, 0, 0, 2, None) == 1001        # height 0
+    b = SirenBatch()
+    b.loss_mode = 7                                                          # not MSE / L1
+    net.hidden = 256
+    assert lib.siren_forward(ctypes.byref(net), ctypes.byref(b), None) in (1001, 1002, 1003)
 
 
 @pytest.mark.parametrize("hidden", [128, 256, 512, 1024])

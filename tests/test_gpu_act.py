@@ -20,6 +20,7 @@ import pytest
 import torch
 
 from oracle import siren_oracle as orc
+from errlog import check_grads, log
 
 pytestmark = pytest.mark.gpu
 
@@ -231,8 +232,7 @@ def test_train_step_act_vs_oracle(dev, H, cfg, n, a0, in_dim, mb):
     out, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
     ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), 1000.0, 30.0, half=True)
     assert set(ref) == set(got)
-    for k, r in ref.items():
-        assert _rel(got[k].reshape(r.shape), r) < 2e-2, k
+    check_grads(f"act_step[{H}x{cfg}x{n}x{in_dim}x{mb}]", got, ref)
     out32, _ = orc.forward(p, t.numpy(), 1000.0, 30.0)
     assert abs(eng.last_loss() - orc.mse(out32, y.numpy())) < 2e-2 * orc.mse(out32, y.numpy())
 

@@ -1,0 +1,62 @@
+"""bench.py's driver contract, run as the driver runs it: one JSON line from rank 0 with the
+BASELINE metric, and -- before the 8-GPU node ever sees it -- the torchrun data-parallel path
+(one process per rank, barrier + max-over-ranks timing, per-layer gradient buckets on a
+communication stream).  On the one-GPU box the two ranks share the card and talk over gloo;
+the node run uses the same code with --backend nccl (RCCL)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(cmd, timeout=240):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _common(res, n, workload):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in res, k
+    assert res["n_gpus"] == n and res["config"]["parallelism"] == f"dp{n}"
+    assert res["value"] > 0 and res["scaling"] == "weak" and res["higher_is_better"] is True
+    assert res["config"]["workload"].startswith(workload)
+    assert res["roofline"]["bound"] == "mfma" and 0 < res["roofline"]["frac"] < 1
+    assert res["fp16_overflow_steps"] == 0
+
+
+def test_torchrun_two_ranks_gloo():
+    res = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                "--backend", "gloo", "--steps", "2", "--warmup", "1", "--coords", "65536", "--hidden", "256",
+                "--layers", "3", "--no-cpu-baseline"])
+    _common(res, 2, "cfg2")
+    assert res["config"]["global_batch"] == 2 * 65536 and res["config"]["backend"] == "gloo"
+    assert "cpu_baseline" not in res
+
+
+@pytest.mark.parametrize("cfg,extra", [("cfg3", ["--coords", "262144"]), ("cfg4", [])])
+def test_single_gpu_configs(cfg, extra):
+    res = _run([sys.executable, "bench.py", "--config", cfg, "--steps", "2", "--warmup", "1",
+                "--no-cpu-baseline", *extra])
+    _common(res, 1, cfg)
+    assert res["config"]["in_features"] == 2
+    assert res["config"]["layers"] == (6 if cfg == "cfg3" else 5)

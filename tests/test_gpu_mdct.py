@@ -11,6 +11,7 @@ import torch
 from scipy.io import wavfile
 
 from oracle import siren_oracle as orc
+from errlog import check_grads
 
 pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -43,9 +44,7 @@ def test_mdct_step_grads_vs_oracle(dev):
     p = orc.Params.from_state_dict(sd0, 4)
     out, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
     ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), 1000.0, 30.0, half=True)
-    for k, r in ref.items():
-        rel = np.linalg.norm(got[k].reshape(r.shape) - r) / np.linalg.norm(r)
-        assert rel < 2e-2, (k, rel)
+    check_grads("mdct_step", got, ref)
 
 
 def test_mdct_fit_first_steps_track_reference(dev):

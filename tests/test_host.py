@@ -135,10 +135,39 @@ def test_waveform_fitting_and_reported_snr(tmp_path):
     assert d2.sample_rate == int(ref2["sample_rate"])
 
 
+@pytest.mark.parametrize("kind", ["f32", "i16"])
+def test_multiwave_fitting_bit_exact(tmp_path, kind):
+    """MultiWaveformFitting (utils.py:186-231, BASELINE cfg3's (t, ch) grid) against the
+    reference's own output (tests/golden/multiwave.npz): channel trim, FIR decimation,
+    height-major (time, channel) coordinates, no normalisation."""
+    from scipy.io import wavfile
+    from inr_for_audio_amd.utils import MultiWaveformFitting, get_coord
+    g = np.load(os.path.join(G, "multiwave.npz"))
+    wav = str(tmp_path / "c.wav")
+    wavfile.write(wav, int(g["fs"]), g[f"clip_{kind}"])
+    for nc in (2, 1):
+        for lp in (False, True):
+            tag = f"{kind}_c{nc}_{'lp' if lp else 'raw'}"
+            ds = MultiWaveformFitting(wav, duration=1, num_channels=nc, lp=lp)
+            coords, samples = ds[0]
+            assert [ds.height, ds.width, ds.sample_rate] == g[f"{tag}_meta"].tolist()
+            assert coords.dtype == torch.float32 and np.array_equal(coords.numpy(), g[f"{tag}_coords"]), tag
+            assert samples.dtype == g[f"{tag}_samples"].dtype
+            assert np.array_equal(samples, g[f"{tag}_samples"]), tag
+            # time column = get_coord(height) repeated per channel; channel column alternates
+            t = get_coord(ds.height, 1).numpy().reshape(-1)
+            assert np.array_equal(coords.numpy()[:, 0], np.repeat(t, ds.width))
+            assert np.array_equal(ds.to_channels(samples.reshape(-1))[:, -1], samples.reshape(-1)[nc - 1::nc])
+    with pytest.raises(IndexError):  # the reference indexes [:T, :nc]: a mono file is rejected
+        mono = str(tmp_path / "m.wav")
+        wavfile.write(mono, int(g["fs"]), g["clip_f32"][:, 0].copy())
+        MultiWaveformFitting(mono, duration=1, num_channels=1)
+
+
 def test_unsupported_train_options_raise(tmp_path):
     from inr_for_audio_amd.run import train
     for kw in (dict(method="mdct", bwe=True), dict(arch="kan", method="mdct"), dict(arch="rbf"),
-               dict(loss_mode="mae"), dict(alpha=0.5)):
+               dict(loss_mode="snr"), dict(alpha=0.5), dict(multichannel=True, bwe=True)):
         with pytest.raises(NotImplementedError):
             train(str(tmp_path), "t", "x", 1, **kw)
     with pytest.raises(ValueError):

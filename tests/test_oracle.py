@@ -201,3 +201,25 @@ def test_act_forward_backward_matches_reference(name):
         r = fb[f"{name}_grad_{k}"]
         rel = np.linalg.norm(np.asarray(g).reshape(r.shape) - r) / np.linalg.norm(r)
         assert rel < 1e-4, (name, k, rel)
+
+
+def test_multiwave_grid_matches_reference_fixture():
+    """oracle.multiwave_grid == the reference MultiWaveformFitting's coordinates
+    (tests/golden/multiwave.npz, utils.py:211-220), one and two channels."""
+    g = np.load(os.path.join(G, "multiwave.npz"))
+    for tag in ("f32_c2_raw", "f32_c1_raw", "f32_c2_lp", "i16_c1_lp"):
+        h, w, _ = g[f"{tag}_meta"].tolist()
+        assert np.array_equal(orc.multiwave_grid(h, w), g[f"{tag}_coords"]), tag
+
+
+def test_l1_grad_is_torch_l1loss_backward():
+    import torch
+    rng = np.random.default_rng(3)
+    out = rng.standard_normal(1000).astype(np.float32)
+    y = out.copy()
+    y[::3] += rng.standard_normal(334).astype(np.float32)   # two thirds of the rows exact: sign 0
+    o = torch.tensor(out, requires_grad=True)
+    loss = torch.nn.L1Loss()(o, torch.tensor(y))
+    loss.backward()
+    assert np.array_equal(o.grad.numpy(), orc.l1_grad(out, y))
+    assert abs(orc.l1(out, y) - float(loss)) < 1e-7
