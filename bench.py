@@ -99,12 +99,104 @@ CONFIGS = {  # name: (hidden, layers, in_dim, coords per GPU, omega0, grid heigh
 }
 
 
+def kan_bytes_per_row(widths):
+    """Algorithmic HBM bytes per coordinate of one KAN training step, per launch kind, for the
+    materialised-expansion design (kan.hip): per layer l (in -> out, A = 9 in fp32 columns)
+      expand   reads X (4 in), writes A (36 in)
+      gemm     reads A, writes X_{l+1} (4 out)
+      dw       reads G (4 out) and A
+      da       reads G, writes dA (36 in)             (l > 0)
+      contract reads X and dA, writes G_l (4 in)      (l > 0)
+    Weights, slabs and partials are O(width^2) per launch, not per row, and left out."""
+    b = {"kan_expand": 0, "kan_gemm": 0, "kan_dw": 0, "kan_da": 0, "kan_contract": 0}
+    for l in range(len(widths) - 1):
+        i, o = widths[l], widths[l + 1]
+        b["kan_expand"] += 4 * i + 36 * i
+        b["kan_gemm"] += 36 * i + 4 * o
+        b["kan_dw"] += 4 * o + 36 * i
+        if l > 0:
+            b["kan_da"] += 4 * o + 36 * i
+            b["kan_contract"] += 4 * i + 36 * i + 4 * i
+    return b
+
+
+def run_kan(args, world, rank, dev, dist, lib, _lib):
+    """cfg5: KAN([1, H, H, 1]) full-batch fit step (KanEngine, siren_kan_train_step)."""
+    from inr_for_audio_amd.engine import KanEngine
+    from inr_for_audio_amd.kan import KAN
+    H = args.hidden or 64
+    per_gpu = args.coords or 441_000
+    n_total = per_gpu * world
+    coords = torch.empty(per_gpu, 1, dtype=torch.float32, device=dev)
+    _lib.check(lib.siren_coords_fill(coords.data_ptr(), per_gpu, rank * per_gpu, n_total,
+                                     torch.cuda.current_stream(dev).cuda_stream), "coords_fill")
+    t = coords[:, 0]
+    target = 0.5 * torch.sin(2300.0 * t) + 0.3 * torch.sin(7100.0 * t + 0.5)
+    torch.manual_seed(0)
+    widths = [1, H, H, 1]
+    eng = KanEngine(KAN(widths), coords, target, n_total=n_total, micro_batch=args.micro_batch or per_gpu,
+                    hist_cap=args.warmup + args.steps + 1, device=dev)
+    for _ in range(args.warmup):
+        eng.step()
+    torch.cuda.synchronize(dev)
+    _lib.check(lib.siren_profile_enable(64 * (args.steps + 1) * eng.n_micro), "profile_enable")
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = _lib.profile_read()
+    _lib.check(lib.siren_profile_enable(0), "profile_disable")
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    rows = per_gpu / eng.n_micro
+    bpr = kan_bytes_per_row(widths)
+    kernels = {}
+    for k, (ms, n) in prof.items():
+        if n:
+            kernels[k] = {"launches_per_step": n / args.steps, "avg_ms": ms / n, "ms_per_step": ms / args.steps}
+            if k in bpr:
+                kernels[k]["bytes_per_step"] = bpr[k] * per_gpu
+                kernels[k]["gbs"] = bpr[k] * per_gpu / (ms / args.steps * 1e-3) / 1e9
+    dom = max((k for k in kernels if k in bpr), key=lambda k: kernels[k]["ms_per_step"])
+    ms_per_step = elapsed / args.steps * 1e3
+    step_bytes = sum(bpr.values()) * per_gpu
+    result = {
+        "metric": METRIC, "value": n_total * args.steps / elapsed, "unit": "coord-samples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic two-tone signal on the linspace(-1, 1) time grid; random-init KAN (seed 0)",
+        "config": {"workload": f"cfg5: KAN({widths}) full-batch fit step, {per_gpu} coords/GPU", "name": "cfg5",
+                   "global_batch": n_total, "coords_per_gpu": per_gpu, "widths": widths,
+                   "micro_batches_per_gpu": eng.n_micro, "parallelism": f"dp{world}",
+                   "backend": args.backend if world > 1 else None},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["gbs"], "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": kernels[dom]["gbs"] / PEAK_HBM_GBS, "traffic": None,
+                     "algorithmic_bytes_per_row": bpr[dom], "rows_per_launch": rows},
+        "step_hbm_frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS,
+        "step_algorithmic_bytes": step_bytes,
+        "kernels": kernels,
+        "final_loss": eng.last_loss(),
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2")
+    ap.add_argument("--config", choices=sorted(CONFIGS) + ["cfg5"], default="cfg2")
     ap.add_argument("--hidden", type=int, default=None, help="override the config's width")
     ap.add_argument("--layers", type=int, default=None, help="SIREN L: sine layers incl. the first")
     ap.add_argument("--coords", type=int, default=None, help="coordinates per GPU (weak scaling)")
@@ -136,6 +228,8 @@ def main():
         torch.cuda.set_device(dev)
         dist.init_process_group(args.backend)
     lib = _lib.load()
+    if args.config == "cfg5":
+        return run_kan(args, world, rank, dev, dist, lib, _lib)
 
     cfg_h, cfg_l, in_dim, cfg_coords, cfg_w0, grid_h = CONFIGS[args.config]
     H = args.hidden or cfg_h

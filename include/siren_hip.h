@@ -302,13 +302,18 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* grads,
 
 /* ---- per-launch HIP-event profiling of the fused path (bench.py) --------------------
  * siren_profile_enable(n) creates 2n hipEvents; while enabled every launch made by
- * siren_train_step / siren_backward / siren_forward / siren_apply_update is bracketed
+ * siren_train_step / siren_backward / siren_forward / siren_apply_update (and the KAN
+ * entry points, kinds 8..13) is bracketed
  * by events on its stream (eager launches only; not meant for graph capture).
  * siren_profile_read sums the elapsed time of all records of one kind (synchronises). */
 enum siren_prof_kind {
   SIREN_PROF_FIRST_FWD = 0, SIREN_PROF_INNER_FWD = 1, SIREN_PROF_HEAD = 2, SIREN_PROF_BWD_DW = 3,
   SIREN_PROF_BWD_DX = 4, SIREN_PROF_BWD_DX0 = 5, SIREN_PROF_REDUCE = 6, SIREN_PROF_UPDATE = 7,
-  SIREN_PROF_NKINDS = 8
+  /* KAN variant (siren_kan_train_step / siren_kan_forward): basis expansion, forward GEMM,
+   * weight-gradient GEMM (+ slab reduce), dA GEMM, contraction, and the small rest */
+  SIREN_PROF_KAN_EXPAND = 8, SIREN_PROF_KAN_GEMM = 9, SIREN_PROF_KAN_DW = 10, SIREN_PROF_KAN_DA = 11,
+  SIREN_PROF_KAN_CONTRACT = 12, SIREN_PROF_KAN_MISC = 13,
+  SIREN_PROF_NKINDS = 14
 };
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
  * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;

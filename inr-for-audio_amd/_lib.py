@@ -159,7 +159,8 @@ _SIGS = {
 
 STRUCTS = [SirenNet, SirenGrads, SirenBatch, SirenOptState, SirenKanNet, SirenKanGrads, SirenKanBatch, SirenGuard]
 
-PROF_KINDS = ["first_fwd", "inner_fwd", "head", "bwd_dw", "bwd_dx", "bwd_dx0", "reduce", "update"]
+PROF_KINDS = ["first_fwd", "inner_fwd", "head", "bwd_dw", "bwd_dx", "bwd_dx0", "reduce", "update",
+              "kan_expand", "kan_gemm", "kan_dw", "kan_da", "kan_contract", "kan_misc"]
 
 
 def profile_read() -> dict:

@@ -654,11 +654,11 @@ hipError_t kan_run_forward(const siren_kan_net* n, const siren_kan_batch* b, con
   for (int l = 0; l < n->n_layers; ++l) {
     const int in = n->width[l], out = n->width[l + 1];
     const int64_t K = (int64_t)KAN_K1 * in;
-    hipError_t e = kan_expand(x, n->grid[l], R, in, w.A[l], s);
-    if (e == hipSuccess) e = kan_combine(n->base_w[l], n->spline_w[l], n->scaler[l], out, in, w.W[l], s);
+    SIREN_PROF(SIREN_PROF_KAN_EXPAND, s, kan_expand(x, n->grid[l], R, in, w.A[l], s));
+    SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_combine(n->base_w[l], n->spline_w[l], n->scaler[l], out, in, w.W[l], s));
     // X[l+1][r][o] = sum_k A[r][k] W[o][k]
-    if (e == hipSuccess) e = kan_gemm(w.A[l], K, 1, w.W[l], 1, K, (int)R, out, K, 1, nullptr, w.X[l + 1], s);
-    if (e != hipSuccess) return e;
+    SIREN_PROF(SIREN_PROF_KAN_GEMM, s, kan_gemm(w.A[l], K, 1, w.W[l], 1, K, (int)R, out, K, 1, nullptr,
+                                                w.X[l + 1], s));
     x = w.X[l + 1];
   }
   return hipSuccess;
@@ -704,9 +704,10 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, si
   SIREN_TRY(hipMemsetAsync(w.zero, 0, sizeof(float), s));
   SIREN_TRY(kan_run_forward(net, b, w, s));
   // MSELoss (run.py:168): out, g = 2(out - y)/N_total, squared-error partials
-  SIREN_TRY(head_loss(w.X[net->n_layers], 1, b->rows, w.zero, b->target, b->n_valid,
-                      (float)(2.0 / b->n_total), b->out, b->g, w.sse_part, w.gsum_part, w.gmax_part, s));
-  SIREN_TRY(sum_to(w.sse_part, (int)((R + 255) / 256), gr->sse, 1, s));
+  SIREN_PROF(SIREN_PROF_KAN_MISC, s, head_loss(w.X[net->n_layers], 1, b->rows, w.zero, b->target, b->n_valid,
+                                               (float)(2.0 / b->n_total), b->out, b->g, w.sse_part, w.gsum_part,
+                                               w.gmax_part, s));
+  SIREN_PROF(SIREN_PROF_KAN_MISC, s, sum_to(w.sse_part, (int)((R + 255) / 256), gr->sse, 1, s));
   // backward (autograd of run.py:185): G = dLoss/dX[l+1], [R][out]
   const float* G = b->g;
   int cur = 0;
@@ -714,13 +715,13 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, si
     const int in = net->width[l], out = net->width[l + 1];
     const int64_t K = (int64_t)KAN_K1 * in;
     // dW[o][k] = sum_r G[r][o] A[r][k]  (split-K over the coordinates)
-    SIREN_TRY(kan_gemm(G, 1, out, w.A[l], K, 1, out, (int)K, R, b->splits, w.slab, w.dW, s));
-    SIREN_TRY(kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1, gr->base_w[l], gr->spline_w[l],
-                              gr->scaler[l], s));
+    SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_gemm(G, 1, out, w.A[l], K, 1, out, (int)K, R, b->splits, w.slab, w.dW, s));
+    SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
+                                                       gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
     if (l == 0) break;
     // dA[r][k] = sum_o G[r][o] W[o][k];  dX = SiLU' dA_base + sum_c B'_c dA_spline_c
-    SIREN_TRY(kan_gemm(G, out, 1, w.W[l], K, 1, (int)R, (int)K, out, 1, nullptr, w.dA, s));
-    SIREN_TRY(kan_contract(w.X[l], net->grid[l], w.dA, R, in, w.G[cur], s));
+    SIREN_PROF(SIREN_PROF_KAN_DA, s, kan_gemm(G, out, 1, w.W[l], K, 1, (int)R, (int)K, out, 1, nullptr, w.dA, s));
+    SIREN_PROF(SIREN_PROF_KAN_CONTRACT, s, kan_contract(w.X[l], net->grid[l], w.dA, R, in, w.G[cur], s));
     G = w.G[cur];
     cur ^= 1;
   }

@@ -36,6 +36,13 @@
 #include "siren_common.h"
 #include "siren_kernels.h"
 
+#ifndef SIREN_XPOL
+#define SIREN_XPOL 0  // cache policy of the X-operand LDS-DMA (glds16_asm_pol; measurement builds)
+#endif
+#ifndef SIREN_WPOL
+#define SIREN_WPOL 0  // ... of the W operand
+#endif
+
 namespace siren {
 
 // Source-side XOR swizzle of a staged [rows][BK] fp16 image (16-B chunks).  BK = 64 (128-B
@@ -477,7 +484,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       const h16* src = ((PC & 1) ? (sel ? x1 : x0) : (sel ? w1 : w0)) + kt * BK;
       const char* dst = smem + slot * Cfg::STAGE;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) glds16_asm(src + psrc[PC][j], lds_addr(dst + pdst[PC][j]));
+      for (int j = 0; j < 2; ++j)
+        glds16_asm_pol<(PC & 1) ? SIREN_XPOL : SIREN_WPOL>(src + psrc[PC][j], lds_addr(dst + pdst[PC][j]));
     };
     h16x8 xf[4][2], wf0[2][2], wf1[2][2];
     auto rd_w = [&](h16x8 (&wf)[2][2], const char* ws, int n_off) {

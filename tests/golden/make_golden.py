@@ -353,6 +353,8 @@ def main():
     ap.add_argument("--trajectory-steps", type=int, default=300)
     ap.add_argument("--fullsize-seeds", default="", help="write only the 5x1024 multi-seed trajectories")
     ap.add_argument("--patience", type=int, default=200)
+    ap.add_argument("--lr", type=float, default=1e-3, help="--fullsize-seeds: Adam lr")
+    ap.add_argument("--fullsize-file", default="trajectory_5x1024_w3000_seeds.json")
     ap.add_argument("--seeds", default="0,1,2,3,4", help="init seeds of the multi-seed trajectories")
     ap.add_argument("--only-seeds", action="store_true", help="write only the multi-seed file")
     ap.add_argument("--only-act", action="store_true", help="write only the Snake / Tanh fixtures")
@@ -383,7 +385,7 @@ def main():
         return
     if args.fullsize_seeds:
         fullsize_seed_trajectories(ref_models, ref_utils, [int(s) for s in args.fullsize_seeds.split(",")],
-                                   args.trajectory_steps, args.patience)
+                                   args.trajectory_steps, args.patience, lr=args.lr, fname=args.fullsize_file)
         return
     if args.only_seeds:
         seed_trajectories(ref_models, ref_utils, [int(s) for s in args.seeds.split(",")],

@@ -53,6 +53,13 @@ def test_torchrun_two_ranks_gloo():
     assert "cpu_baseline" not in res
 
 
+def test_kan_config():
+    res = _run([sys.executable, "bench.py", "--config", "cfg5", "--steps", "2", "--warmup", "1", "--coords", "50000"])
+    assert res["n_gpus"] == 1 and res["value"] > 0 and res["dtype"] == "fp32"
+    assert res["config"]["widths"] == [1, 64, 64, 1] and res["roofline"]["bound"] == "hbm"
+    assert 0 < res["roofline"]["frac"] < 1 and res["roofline"]["kernel"].startswith("kan_")
+
+
 @pytest.mark.parametrize("cfg,extra", [("cfg3", ["--coords", "262144"]), ("cfg4", [])])
 def test_single_gpu_configs(cfg, extra):
     res = _run([sys.executable, "bench.py", "--config", cfg, "--steps", "2", "--warmup", "1",
