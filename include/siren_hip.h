@@ -329,8 +329,9 @@ enum siren_prof_kind {
  * values so every block walks several tiles);
  * SIREN_OPT_NT_DIAG = measurement-only NT ablations (results are WRONG while set): bit 0 reads
  *   the X operand from the first 4 row bands only (L2-resident operand); ping-pong K-loop
- *   (pipe 4) only: bit 9 runs no tiles, bit 10 skips the epilogue (its compute and stores).
- *   (Bits 1-3 -- no stores, identity sin/cos, non-temporal stores -- were retired in r06: their
+ *   (pipe 4) only: bit 2 reads W from column tile 0 only (L2-resident W), bit 9 runs no tiles,
+ *   bit 10 skips the epilogue (its compute and stores).
+ *   (The r05 bits 1-3 -- no stores, identity sin/cos, non-temporal stores -- were retired in r06: their
  *   per-store branches cost the production epilogue; DESIGN.md keeps their measurements);
  * SIREN_OPT_NT_STAGGER = persistent NT start stagger: block b idles (b % 16) * value units of
  * ~1.7k cycles before its first tile, so that the blocks' epilogue store bursts do not

@@ -537,7 +537,7 @@ int siren_set_option(int32_t option, int32_t value) {
       gemm_nt_set_pf_dist(value);
       return SIREN_OK;
     case SIREN_OPT_NT_DIAG:
-      if (value < 0 || (value & ~(1 | 512 | 1024))) return SIREN_ERR_CONFIG;
+      if (value < 0 || (value & ~(1 | 4 | 512 | 1024))) return SIREN_ERR_CONFIG;
       gemm_nt_set_diag(value);
       return SIREN_OK;
     case SIREN_OPT_NT_STAGGER:

@@ -474,7 +474,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         tile_of(t, m0, n0);
         const int xm0 = (p.diag & 1) ? (m0 & (4 * BM - 1)) : m0;
         xb = p.X + (size_t)xm0 * K;
-        wb = p.W + (size_t)n0 * K;
+        wb = p.W + (size_t)((p.diag & 4) ? 0 : n0) * K;  // diag bit 2: one W column tile (L2-resident W)
       };
       bases(ti, x0, w0);
       bases(ti + 1 < my_tiles ? ti + 1 : ti, x1, w1);

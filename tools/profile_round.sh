@@ -4,6 +4,8 @@
 #   trace/                  rocprofv3 --kernel-trace --stats of a short bench run
 #   bench_pmc_hbm.json      FETCH_SIZE and WRITE_SIZE, each in its own --pmc pass
 #   bench_pmc_mfma.json     SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE: MFMA utilisation per kernel
+#   bench_cfg{3,4,5}.json   the other BASELINE configs' bench lines; trace_cfg{3,4,5}/ their
+#                           rocprofv3 --kernel-trace --stats
 # Every GPU step has its own time limit and the steps are chained with &&.
 #   bash tools/profile_round.sh r02
 set -euo pipefail
@@ -23,5 +25,10 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_wr
 timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mfma" -o run -- \
   python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_mfma.log" 2>&1 &&
 python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_hbm.json" "$OUT/pmc_fetch" "$OUT/pmc_write" &&
-python3 "$ROOT/tools/pmc_mfma.py" "$OUT/bench_pmc_mfma.json" "$OUT/pmc_mfma"
+python3 "$ROOT/tools/pmc_mfma.py" "$OUT/bench_pmc_mfma.json" "$OUT/pmc_mfma" &&
+for c in cfg3 cfg4 cfg5; do
+  timeout -k 10 300 python3 "$ROOT/bench.py" --config $c --no-cpu-baseline > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" &&
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$c" -o run -- \
+    python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/trace_$c.log" 2>&1 || exit 3
+done
 echo "profile $TAG done"
