@@ -157,3 +157,32 @@ def test_fit_quality_headline_model_over_seeds(dev):
           f"lr drops GPU {drops_gpu} reference {drops_ref}")
     assert drops_ref > 0 and drops_gpu > 0
     assert _envelope(med(best_gpu), med(best_ref), med(best_t32))
+
+
+def test_fit_headline_model_stable_regime_per_seed(dev):
+    """SIREN 5x1024, omega0 = 3000, gt_bach 1 s at lr 3e-5 (tests/golden/
+    trajectory_5x1024_w3000_lr3e-5_seeds.json): a regime where the reference's trajectory does not
+    depend on summation order (two CPU thread counts agree to 1.2e-5 in every step's loss over 40
+    steps), so the HIP path can be held to north_star's 0.1 dB per seed, not as a median: the
+    whole 150-step loss trajectory tracks the reference and each seed's final SNR (the fit of the
+    final weights to the target) is within 0.1 dB."""
+    from inr_for_audio_amd.utils import calculate_snr
+    ref = json.load(open(os.path.join(G, "trajectory_5x1024_w3000_lr3e-5_seeds.json")))
+    var = float(np.mean(np.load(os.path.join(G, "gt_bach_1s.npz"))["target"].astype(np.float64) ** 2))
+    rows = {}
+    for s in sorted(int(k) for k in ref["runs"]):
+        r = ref["runs"][str(s)]
+        eng, out, snr = _fit(dev, ref["steps"], seed=s, H=1024, L=4, w0=ref["omega0"], lr=ref["lr0"],
+                             patience=ref["patience"])
+        losses, lrs = eng.history()
+        rl = np.array(r["loss"])
+        dev_db = np.abs(10 * np.log10(losses / rl))
+        rows[s] = {"final_snr_gpu": snr, "final_snr_ref": r["snr_target"], "max_step_db": float(dev_db.max()),
+                   "best_gpu": _db(var, np.min(losses)), "best_ref": _db(var, np.min(rl))}
+        assert np.array_equal(lrs, np.array(r["lr"])), s
+    log("fit_5x1024_stable", seeds=rows)
+    print("\n" + json.dumps(rows, indent=1))
+    for s, v in rows.items():
+        assert abs(v["final_snr_gpu"] - v["final_snr_ref"]) < 0.1, (s, v)
+        assert abs(v["best_gpu"] - v["best_ref"]) < 0.1, (s, v)
+        assert v["max_step_db"] < 0.1, (s, v)
