@@ -259,6 +259,28 @@ int siren_plateau_step(siren_opt_state* state, const float* sse, double n_total,
 int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wh, uint16_t* WTh,
                       void* stream);
 
+/* ---- unfused fp32 layers: the module API outside the fused step ------------------------
+ * A lone SineLayer (models.py:114-120: forward, forward_with_intermediate), nn.Linear, Snake
+ * (models.py:235-241) and nn.Tanh -- what SirenWithSnakeTanh.forward_with_activations
+ * (models.py:396-423) walks -- in fp32 like the reference (the fused path stores fp16).
+ * x [rows][in], W [out][in] (nn.Linear layout), b [out] or NULL; all fp32, row-major. */
+enum siren_fp32_act { SIREN_FP32_IDENTITY = 0, SIREN_FP32_SIN = 1, SIREN_FP32_TANH = 2, SIREN_FP32_SNAKE = 3 };
+/* pre = omega * (x W^T + b)  (models.py:115 `self.omega_0 * self.linear(input)`; omega 1: nn.Linear) */
+int siren_fp32_linear(const float* x, int64_t rows, int32_t in, int32_t out, const float* W, const float* b,
+                      float omega, float* pre, void* stream);
+/* y = act(x) elementwise over [rows][cols]: sin (models.py:115), tanh, Snake x + sin^2(a x)/a with a [cols] */
+int siren_fp32_act(int32_t act, const float* x, int64_t rows, int32_t cols, const float* a, float* y, void* stream);
+/* autograd of siren_fp32_act for dL/dy = gy: gx = gy * act'(x); Snake also da [cols] = column sums of
+ * gy * dy/da (da_prod: rows*cols floats of scratch, tmp: 64*cols floats; both NULL otherwise) */
+int siren_fp32_act_bwd(int32_t act, const float* x, int64_t rows, int32_t cols, const float* a, const float* gy,
+                       float* gx, float* da, float* da_prod, float* tmp, void* stream);
+/* autograd of siren_fp32_linear for dL/dpre = gpre (overwritten with omega * gpre): gW [out][in] via
+ * `splits` split-K slices over the rows into `slab` (splits*out*in floats), gb [out] and gx [rows][in]
+ * (either NULL: not computed); tmp: 64*out floats */
+int siren_fp32_linear_bwd(const float* x, int64_t rows, int32_t in, int32_t out, const float* W, float omega,
+                          float* gpre, float* gx, float* gW, float* gb, float* slab, int32_t splits, float* tmp,
+                          void* stream);
+
 /* ---- KAN variant: run.py:92-93 KAN([in, H, H, 1]) of kan.py:169-285 ----------
  * Layer l maps width[l] -> width[l+1] as efficient-KAN's KANLinear (kan.py:6-166) with
  * grid_size 5, spline_order 3, SiLU base: out = SiLU(x) base_w^T + B(x) (spline_w*scaler)^T,

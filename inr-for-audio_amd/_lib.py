@@ -17,6 +17,7 @@ ABI_VERSION = 5
 MAX_INNER = 16
 ROW_TILE = 128
 ACT_SINE, ACT_SNAKE, ACT_TANH = 0, 1, 2  # siren_act
+FP32_IDENTITY, FP32_SIN, FP32_TANH, FP32_SNAKE = 0, 1, 2, 3  # siren_fp32_act
 
 _p = ctypes.c_void_p
 _f32p = ctypes.POINTER(ctypes.c_float)
@@ -147,6 +148,11 @@ _SIGS = {
     "siren_plateau_step": (ctypes.c_int, [_p, _p, ctypes.c_double, _p, _p, _i64, _p]),
     "siren_cast_weight": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p]),
     "siren_set_option": (ctypes.c_int, [_i32, _i32]),
+    "siren_fp32_linear": (ctypes.c_int, [_p, _i64, _i32, _i32, _p, _p, ctypes.c_float, _p, _p]),
+    "siren_fp32_act": (ctypes.c_int, [_i32, _p, _i64, _i32, _p, _p, _p]),
+    "siren_fp32_act_bwd": (ctypes.c_int, [_i32, _p, _i64, _i32, _p, _p, _p, _p, _p, _p, _p]),
+    "siren_fp32_linear_bwd": (ctypes.c_int, [_p, _i64, _i32, _i32, _p, ctypes.c_float, _p, _p, _p, _p, _p, _i32, _p,
+                                              _p]),
     "siren_kan_workspace_floats": (_i64, [ctypes.POINTER(SirenKanNet), _i32, _i32]),
     "siren_kan_forward": (ctypes.c_int, [ctypes.POINTER(SirenKanNet), ctypes.POINTER(SirenKanBatch), _p]),
     "siren_kan_train_step": (ctypes.c_int, [ctypes.POINTER(SirenKanNet), ctypes.POINTER(SirenKanGrads),

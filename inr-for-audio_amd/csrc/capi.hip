@@ -9,6 +9,8 @@ using namespace siren;
 
 static_assert(sizeof(siren_opt_state) == sizeof(OptState), "opt state layout");
 static_assert(sizeof(siren_guard) == sizeof(GuardState), "guard layout");
+static_assert((int)SIREN_FP32_SNAKE == (int)siren::FP32_SNAKE && (int)SIREN_FP32_SIN == (int)siren::FP32_SIN &&
+                  (int)SIREN_FP32_TANH == (int)siren::FP32_TANH, "fp32 act codes");
 
 namespace {
 
@@ -511,6 +513,43 @@ int siren_cast_weight(const float* W, int32_t h_out, int32_t h_in, uint16_t* Wh,
   if (!W || !Wh || !WTh) return SIREN_ERR_NULL;
   if (h_out % 64 || h_in % 64) return SIREN_ERR_SHAPE;
   return (int)cast_weight(W, h_out, h_in, B(Wh), B(WTh), S(stream));
+}
+
+int siren_fp32_linear(const float* x, int64_t rows, int32_t in, int32_t out, const float* W, const float* b,
+                      float omega, float* pre, void* stream) {
+  if (!x || !W || !pre) return SIREN_ERR_NULL;
+  if (rows < 1 || rows > INT32_MAX || in < 1 || out < 1) return SIREN_ERR_SHAPE;
+  return (int)fp32_linear(x, rows, in, out, W, b, omega, pre, S(stream));
+}
+
+static bool fp32_act_ok(int32_t act) { return act >= SIREN_FP32_IDENTITY && act <= SIREN_FP32_SNAKE; }
+
+int siren_fp32_act(int32_t act, const float* x, int64_t rows, int32_t cols, const float* a, float* y, void* stream) {
+  if (!fp32_act_ok(act)) return SIREN_ERR_CONFIG;
+  if (!x || !y || (act == SIREN_FP32_SNAKE && !a)) return SIREN_ERR_NULL;
+  if (rows < 0 || cols < 1) return SIREN_ERR_SHAPE;
+  return (int)fp32_act(act, x, rows, cols, a, y, S(stream));
+}
+
+int siren_fp32_act_bwd(int32_t act, const float* x, int64_t rows, int32_t cols, const float* a, const float* gy,
+                       float* gx, float* da, float* da_prod, float* tmp, void* stream) {
+  if (!fp32_act_ok(act)) return SIREN_ERR_CONFIG;
+  if (!x || !gy || !gx) return SIREN_ERR_NULL;
+  if (act == SIREN_FP32_SNAKE && (!a || (da && (!da_prod || !tmp)))) return SIREN_ERR_NULL;
+  if (rows < 1 || rows > INT32_MAX || cols < 1) return SIREN_ERR_SHAPE;
+  hipStream_t s = S(stream);
+  const bool want_da = act == SIREN_FP32_SNAKE && da;
+  SIREN_TRY(fp32_act_bwd(act, x, rows, cols, a, gy, gx, want_da ? da_prod : nullptr, s));
+  if (want_da) SIREN_TRY(col_reduce(da_prod, cols, (int)rows, cols, da, 1, 0, tmp, s));
+  return SIREN_OK;
+}
+
+int siren_fp32_linear_bwd(const float* x, int64_t rows, int32_t in, int32_t out, const float* W, float omega,
+                          float* gpre, float* gx, float* gW, float* gb, float* slab, int32_t splits, float* tmp,
+                          void* stream) {
+  if (!x || !W || !gpre || !gW || (splits > 1 && !slab) || (gb && !tmp)) return SIREN_ERR_NULL;
+  if (rows < 1 || rows > INT32_MAX || in < 1 || out < 1 || splits < 1) return SIREN_ERR_SHAPE;
+  return (int)fp32_linear_bwd(x, rows, in, out, W, omega, gpre, gx, gW, gb, slab, splits, tmp, S(stream));
 }
 
 int siren_set_option(int32_t option, int32_t value) {

@@ -113,6 +113,16 @@ hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_h
 hipError_t col_reduce(const float* part, int64_t row_stride, int nrows, int ncols, float* out,
                       int out_stride, int accumulate, float* tmp, hipStream_t s);
 
+// unfused fp32 layers (layer_fp32.hip): lone SineLayer / Linear / Snake / Tanh modules
+enum Fp32Act { FP32_IDENTITY = 0, FP32_SIN = 1, FP32_TANH = 2, FP32_SNAKE = 3 };  // == siren_fp32_act
+hipError_t fp32_linear(const float* x, int64_t rows, int in, int out, const float* W, const float* b, float omega,
+                       float* pre, hipStream_t s);
+hipError_t fp32_act(int act, const float* x, int64_t rows, int cols, const float* a, float* y, hipStream_t s);
+hipError_t fp32_act_bwd(int act, const float* x, int64_t rows, int cols, const float* a, const float* gy,
+                        float* gpre, float* da_prod, hipStream_t s);
+hipError_t fp32_linear_bwd(const float* x, int64_t rows, int in, int out, const float* W, float omega, float* gpre,
+                           float* gx, float* gW, float* gb, float* slab, int splits, float* tmp, hipStream_t s);
+
 // KAN (kan.hip): fp32, grid_size 5, spline_order 3 (9 A-columns per input)
 hipError_t kan_expand(const float* X, const float* grid, int64_t N, int in, float* A, hipStream_t s);
 hipError_t kan_contract(const float* X, const float* grid, const float* dA, int64_t N, int in, float* dX,

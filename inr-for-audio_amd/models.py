@@ -43,11 +43,16 @@ class SineLayer(nn.Module):
                                             np.sqrt(6 / self.in_features) / self.omega_0)
 
     def forward(self, input):
-        raise NotImplementedError(
-            "a lone SineLayer has no HIP kernel: wrap it in SirenWithSnakeTanh (fused path)")
+        """sin(omega_0 * linear(input)) -- models.py:114-115, on the unfused fp32 HIP layer kernels
+        (siren_fp32_linear / siren_fp32_act, differentiable).  Inside SirenWithSnakeTanh the
+        fused fp16 path runs instead."""
+        return self.forward_with_intermediate(input)[0]
 
     def forward_with_intermediate(self, input):
-        raise NotImplementedError("activation inspection is not part of the HIP path")
+        """(sin(intermediate), intermediate) with intermediate = omega_0 * linear(input) --
+        models.py:117-120 (activation inspection), fp32 on the GPU."""
+        intermediate = fp32_linear(input, self.linear.weight, self.linear.bias, float(self.omega_0))
+        return fp32_act(intermediate, _lib.FP32_SIN), intermediate
 
 
 class Snake(nn.Module):
@@ -70,8 +75,10 @@ class Snake(nn.Module):
         self.a.requiresGrad = trainable
 
     def forward(self, x):
-        raise NotImplementedError("a lone Snake has no HIP kernel: wrap it in SirenWithSnakeTanh "
-                                  "(fused Linear + Snake epilogue)")
+        """x + sin^2(a x)/a elementwise (models.py:235-241) on the fp32 HIP kernel
+        (siren_fp32_act, differentiable in x and a).  Inside SirenWithSnakeTanh the Linear +
+        Snake pair runs as one fused fp16 GEMM epilogue instead."""
+        return fp32_act(x, _lib.FP32_SNAKE, self.a)
 
 
 class SirenWithSnakeTanh(nn.Module):
@@ -171,6 +178,40 @@ class SirenWithSnakeTanh(nn.Module):
             idx["wh"], idx["bh"] = pos[f"net.{j}.linear.weight"], pos[f"net.{j}.linear.bias"]
         return idx
 
+    def forward_with_activations(self, coords, retain_grad=False):
+        """models.py:396-423: the output of every layer, plus each SineLayer's intermediate
+        omega * linear(x), keyed like the reference ('<class ...>_<count>').  Visualisation
+        only, so it walks the modules one by one on the unfused fp32 HIP kernels (SineLayer /
+        Snake forward, siren_fp32_linear for nn.Linear, siren_fp32_act for nn.Tanh) -- the fp32
+        values the reference reports, not the fused path's fp16 activations."""
+        from collections import OrderedDict
+        if not coords.is_cuda:
+            raise RuntimeError("forward_with_activations runs on the HIP path only (CUDA tensors)")
+        activations = OrderedDict()
+        count = 0
+        x = coords.clone().detach().requires_grad_(True)
+        activations["input"] = x
+        for layer in self.net:
+            if isinstance(layer, SineLayer):
+                x, intermed = layer.forward_with_intermediate(x)
+                if retain_grad:
+                    x.retain_grad()
+                    intermed.retain_grad()
+                activations["_".join((str(layer.__class__), "%d" % count))] = intermed
+                count += 1
+            else:
+                if isinstance(layer, nn.Linear):
+                    x = fp32_linear(x, layer.weight, layer.bias, 1.0)
+                elif isinstance(layer, nn.Tanh):
+                    x = fp32_act(x, _lib.FP32_TANH)
+                else:
+                    x = layer(x)
+                if retain_grad:
+                    x.retain_grad()
+            activations["_".join((str(layer.__class__), "%d" % count))] = x
+            count += 1
+        return activations
+
     def forward(self, coords):
         """(1, N, in) or (N, in) CUDA coords -> (..., N, 1) fp32 output, differentiable in the
         parameters (models.py:388-394)."""
@@ -246,3 +287,100 @@ class _SirenFunction(torch.autograd.Function):
                    "siren_backward")
         ctx.keep = None
         return (None, None, *views)
+
+
+# ---- unfused fp32 layers (layer_fp32.hip): the module API outside the fused step ----------
+def _splits(rows: int) -> int:
+    return max(1, min(256, rows // 2048))
+
+
+class _Fp32Linear(torch.autograd.Function):
+    """pre = omega * (x W^T + b) in fp32 (siren_fp32_linear) and its autograd
+    (siren_fp32_linear_bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, omega):
+        lib = _lib.load()
+        lead = x.shape[:-1]
+        xs = x.reshape(-1, x.shape[-1]).contiguous().float()
+        rows, fin = xs.shape
+        out = W.shape[0]
+        pre = torch.empty(rows, out, dtype=torch.float32, device=x.device)
+        s = torch.cuda.current_stream(x.device).cuda_stream
+        _lib.check(lib.siren_fp32_linear(_lib.ptr(xs), rows, fin, out, _lib.ptr(W.detach().contiguous()),
+                                         _lib.ptr(None if b is None else b.detach().contiguous()),
+                                         float(omega), _lib.ptr(pre), s), "siren_fp32_linear")
+        ctx.save_for_backward(xs, W, b if b is not None else torch.empty(0, device=x.device))
+        ctx.has_b, ctx.omega, ctx.lead = b is not None, float(omega), lead
+        return pre.reshape(*lead, out)
+
+    @staticmethod
+    def backward(ctx, gpre):
+        lib = _lib.load()
+        xs, W, b = ctx.saved_tensors
+        rows, fin = xs.shape
+        out = W.shape[0]
+        dev = xs.device
+        g = gpre.reshape(rows, out).contiguous().float().clone()  # overwritten with omega * gpre
+        gW = torch.empty(out, fin, dtype=torch.float32, device=dev)
+        gb = torch.empty(out, dtype=torch.float32, device=dev) if ctx.has_b else None
+        gx = torch.empty(rows, fin, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
+        splits = _splits(rows)
+        slab = torch.empty(splits * out * fin if splits > 1 else 1, dtype=torch.float32, device=dev)
+        tmp = torch.empty(64 * out, dtype=torch.float32, device=dev)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(lib.siren_fp32_linear_bwd(_lib.ptr(xs), rows, fin, out, _lib.ptr(W.detach().contiguous()),
+                                             ctx.omega, _lib.ptr(g), _lib.ptr(gx), _lib.ptr(gW), _lib.ptr(gb),
+                                             _lib.ptr(slab), splits, _lib.ptr(tmp), s), "siren_fp32_linear_bwd")
+        return (None if gx is None else gx.reshape(*ctx.lead, fin)), gW, gb, None
+
+
+class _Fp32Act(torch.autograd.Function):
+    """y = act(x) elementwise in fp32 (siren_fp32_act) and its autograd (siren_fp32_act_bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, act, a):
+        lib = _lib.load()
+        xs = x.contiguous().float()
+        cols = xs.shape[-1]
+        rows = xs.numel() // cols
+        y = torch.empty_like(xs)
+        s = torch.cuda.current_stream(x.device).cuda_stream
+        ac = None if a is None else a.detach().reshape(-1).contiguous().float()
+        _lib.check(lib.siren_fp32_act(int(act), _lib.ptr(xs), rows, cols, _lib.ptr(ac), _lib.ptr(y), s),
+                   "siren_fp32_act")
+        ctx.save_for_backward(xs, ac if ac is not None else torch.empty(0, device=x.device))
+        ctx.act, ctx.has_a = int(act), a is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        lib = _lib.load()
+        xs, ac = ctx.saved_tensors
+        cols = xs.shape[-1]
+        rows = xs.numel() // cols
+        g = gy.contiguous().float()
+        gx = torch.empty_like(xs)
+        want_da = ctx.has_a and ctx.needs_input_grad[2]
+        da = torch.empty(cols, dtype=torch.float32, device=xs.device) if want_da else None
+        prod = torch.empty_like(xs) if want_da else None
+        tmp = torch.empty(64 * cols, dtype=torch.float32, device=xs.device) if want_da else None
+        s = torch.cuda.current_stream(xs.device).cuda_stream
+        _lib.check(lib.siren_fp32_act_bwd(ctx.act, _lib.ptr(xs), rows, cols, _lib.ptr(ac if ctx.has_a else None),
+                                          _lib.ptr(g), _lib.ptr(gx), _lib.ptr(da), _lib.ptr(prod), _lib.ptr(tmp), s),
+                   "siren_fp32_act_bwd")
+        return gx, None, da
+
+
+def fp32_linear(x, weight, bias, omega=1.0):
+    """omega * (x W^T + b) on the fp32 HIP kernels (x [..., in] CUDA)."""
+    if not x.is_cuda:
+        raise RuntimeError("the HIP layer kernels take CUDA tensors (no CPU fallback)")
+    return _Fp32Linear.apply(x, weight, bias, float(omega))
+
+
+def fp32_act(x, act, a=None):
+    """elementwise sin / tanh / Snake(a) / identity on the fp32 HIP kernel (x CUDA)."""
+    if not x.is_cuda:
+        raise RuntimeError("the HIP layer kernels take CUDA tensors (no CPU fallback)")
+    return _Fp32Act.apply(x, act, a)
