@@ -99,25 +99,30 @@ CONFIGS = {  # name: (hidden, layers, in_dim, coords per GPU, omega0, grid heigh
 }
 
 
-def kan_bytes_per_row(widths):
-    """Algorithmic HBM bytes per coordinate of one KAN training step, per launch kind, for the
-    materialised-expansion design (kan.hip): per layer l (in -> out, A = 9 in fp32 columns)
-      expand   reads X (4 in), writes A (36 in)
-      gemm     reads A, writes X_{l+1} (4 out)
-      dw       reads G (4 out) and A
-      da       reads G, writes dA (36 in)             (l > 0)
-      contract reads X and dA, writes G_l (4 in)      (l > 0)
+PEAK_F32_TFLOPS = 157.3   # MI355X dense fp32 (f32-input MFMA = the vector rate; MI355X_MICROARCH.md)
+
+
+def kan_work_per_row(widths):
+    """Algorithmic work per coordinate of one KAN training step, per launch kind, for the fused
+    design (kan.hip): bytes (activations in and out; the expansions A / dA are recomputed in LDS,
+    never stored) and GEMM flops (2 x 9 in x out per layer and GEMM; the B-spline recursion's own
+    VALU work is not counted, so the flop fraction is a lower bound).  Per layer l (in -> out):
+      kan_fwd  reads X_l (4 in), writes X_{l+1} (4 out);           2*9*in*out flop
+      kan_dw   reads X_l and G_{l+1} (4 out);                       2*9*in*out flop
+      kan_dx   reads X_l, G_{l+1}, writes G_l (4 in)   (l > 0);     2*9*in*out flop
     Weights, slabs and partials are O(width^2) per launch, not per row, and left out."""
-    b = {"kan_expand": 0, "kan_gemm": 0, "kan_dw": 0, "kan_da": 0, "kan_contract": 0}
+    by = {"kan_fwd": 0, "kan_dw": 0, "kan_dx": 0}
+    fl = {"kan_fwd": 0, "kan_dw": 0, "kan_dx": 0}
     for l in range(len(widths) - 1):
         i, o = widths[l], widths[l + 1]
-        b["kan_expand"] += 4 * i + 36 * i
-        b["kan_gemm"] += 36 * i + 4 * o
-        b["kan_dw"] += 4 * o + 36 * i
+        by["kan_fwd"] += 4 * i + 4 * o
+        by["kan_dw"] += 4 * i + 4 * o
+        fl["kan_fwd"] += 18 * i * o
+        fl["kan_dw"] += 18 * i * o
         if l > 0:
-            b["kan_da"] += 4 * o + 36 * i
-            b["kan_contract"] += 4 * i + 36 * i + 4 * i
-    return b
+            by["kan_dx"] += 4 * i + 4 * o + 4 * i
+            fl["kan_dx"] += 18 * i * o
+    return by, fl
 
 
 def run_kan(args, world, rank, dev, dist, lib, _lib):
@@ -157,17 +162,20 @@ def run_kan(args, world, rank, dev, dist, lib, _lib):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     rows = per_gpu / eng.n_micro
-    bpr = kan_bytes_per_row(widths)
+    bpr, fpr = kan_work_per_row(widths)
     kernels = {}
     for k, (ms, n) in prof.items():
         if n:
             kernels[k] = {"launches_per_step": n / args.steps, "avg_ms": ms / n, "ms_per_step": ms / args.steps}
             if k in bpr:
+                sec = ms / args.steps * 1e-3
                 kernels[k]["bytes_per_step"] = bpr[k] * per_gpu
-                kernels[k]["gbs"] = bpr[k] * per_gpu / (ms / args.steps * 1e-3) / 1e9
+                kernels[k]["gbs"] = bpr[k] * per_gpu / sec / 1e9
+                kernels[k]["tflops"] = fpr[k] * per_gpu / sec / 1e12
     dom = max((k for k in kernels if k in bpr), key=lambda k: kernels[k]["ms_per_step"])
     ms_per_step = elapsed / args.steps * 1e3
     step_bytes = sum(bpr.values()) * per_gpu
+    step_flops = sum(fpr.values()) * per_gpu
     result = {
         "metric": METRIC, "value": n_total * args.steps / elapsed, "unit": "coord-samples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
@@ -177,11 +185,17 @@ def run_kan(args, world, rank, dev, dist, lib, _lib):
                    "global_batch": n_total, "coords_per_gpu": per_gpu, "widths": widths,
                    "micro_batches_per_gpu": eng.n_micro, "parallelism": f"dp{world}",
                    "backend": args.backend if world > 1 else None},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["gbs"], "peak": PEAK_HBM_GBS,
-                     "unit": "GB/s", "frac": kernels[dom]["gbs"] / PEAK_HBM_GBS, "traffic": None,
-                     "algorithmic_bytes_per_row": bpr[dom], "rows_per_launch": rows},
+        # compute-bound once the expansions stay on chip: the fp32 dense peak for the dtype
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": kernels[dom]["tflops"], "peak": PEAK_F32_TFLOPS,
+                     "unit": "TFLOP/s", "frac": kernels[dom]["tflops"] / PEAK_F32_TFLOPS, "traffic": None,
+                     "peak_note": "fp32 dense (f32 MFMA = vector rate); the kernels issue fp32 VALU FMAs; "
+                                  "GEMM flops only (the B-spline recursion is extra VALU work)",
+                     "flops_per_row": fpr[dom], "rows_per_launch": rows,
+                     "hbm": {"achieved": kernels[dom]["gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": kernels[dom]["gbs"] / PEAK_HBM_GBS, "algorithmic_bytes_per_row": bpr[dom]}},
+        "step_flop_frac": step_flops / (ms_per_step * 1e-3) / 1e12 / PEAK_F32_TFLOPS,
         "step_hbm_frac": step_bytes / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS,
-        "step_algorithmic_bytes": step_bytes,
+        "step_algorithmic_bytes": step_bytes, "step_gemm_flops": step_flops,
         "kernels": kernels,
         "final_loss": eng.last_loss(),
     }

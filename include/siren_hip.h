@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 5
+#define SIREN_ABI_VERSION 6
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 
@@ -286,8 +286,8 @@ int siren_fp32_linear_bwd(const float* x, int64_t rows, int32_t in, int32_t out,
  * grid_size 5, spline_order 3, SiLU base: out = SiLU(x) base_w^T + B(x) (spline_w*scaler)^T,
  * B = the 8 order-3 B-spline bases on the layer's `grid` buffer [in][12].  fp32 throughout.
  * The last width must be 1.  Workspace: one caller-owned fp32 buffer of
- * siren_kan_workspace_floats(net, rows, splits) floats (activations, expansions, combined
- * weights, split-K slabs). */
+ * siren_kan_workspace_floats(net, rows, splits) floats (activations, combined weights,
+ * gradients of the layer outputs, split-K slabs -- the expansions are never stored). */
 #define SIREN_KAN_MAX_LAYERS 8
 typedef struct siren_kan_net {
   int32_t n_layers, pad0;
@@ -331,11 +331,10 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* grads,
 enum siren_prof_kind {
   SIREN_PROF_FIRST_FWD = 0, SIREN_PROF_INNER_FWD = 1, SIREN_PROF_HEAD = 2, SIREN_PROF_BWD_DW = 3,
   SIREN_PROF_BWD_DX = 4, SIREN_PROF_BWD_DX0 = 5, SIREN_PROF_REDUCE = 6, SIREN_PROF_UPDATE = 7,
-  /* KAN variant (siren_kan_train_step / siren_kan_forward): basis expansion, forward GEMM,
-   * weight-gradient GEMM (+ slab reduce), dA GEMM, contraction, and the small rest */
-  SIREN_PROF_KAN_EXPAND = 8, SIREN_PROF_KAN_GEMM = 9, SIREN_PROF_KAN_DW = 10, SIREN_PROF_KAN_DA = 11,
-  SIREN_PROF_KAN_CONTRACT = 12, SIREN_PROF_KAN_MISC = 13,
-  SIREN_PROF_NKINDS = 14
+  /* KAN variant (siren_kan_train_step / siren_kan_forward): fused forward layer, fused
+   * weight gradient (+ slab reduce), fused dA + contraction, and the small rest */
+  SIREN_PROF_KAN_FWD = 8, SIREN_PROF_KAN_DW = 9, SIREN_PROF_KAN_DX = 10, SIREN_PROF_KAN_MISC = 11,
+  SIREN_PROF_NKINDS = 12
 };
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
  * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;

@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_INNER = 16
 ROW_TILE = 128
 ACT_SINE, ACT_SNAKE, ACT_TANH = 0, 1, 2  # siren_act
@@ -166,7 +166,7 @@ _SIGS = {
 STRUCTS = [SirenNet, SirenGrads, SirenBatch, SirenOptState, SirenKanNet, SirenKanGrads, SirenKanBatch, SirenGuard]
 
 PROF_KINDS = ["first_fwd", "inner_fwd", "head", "bwd_dw", "bwd_dx", "bwd_dx0", "reduce", "update",
-              "kan_expand", "kan_gemm", "kan_dw", "kan_da", "kan_contract", "kan_misc"]
+              "kan_fwd", "kan_dw", "kan_dx", "kan_misc"]
 
 
 def profile_read() -> dict:

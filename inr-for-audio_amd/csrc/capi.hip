@@ -643,14 +643,14 @@ int check_kan(const siren_kan_net* n) {
 }
 
 // Workspace carve-up (floats, each piece 64-float aligned):
-//   A[l] rows x 9 w[l];  X[l] rows x w[l] for l = 1..L (X[L] = the output row vector);
-//   W[l] w[l+1] x 9 w[l];  dW w_max_out x 9 w_max_in;  slab splits x that;  dA rows x 9 w_max;
-//   G[2] rows x w_max;  sse/gsum/gmax partials 3 x ceil(rows/256);  one zero float.
+//   X[l] rows x w[l] for l = 1..L (X[L] = the output row vector);  W[l] w[l+1] x 9 w[l];
+//   dW w_max_out x 9 w_max_in;  slab splits x that;  G[2] rows x w_max;
+//   sse/gsum/gmax partials 3 x ceil(rows/256);  one zero float.
+// (No expansion A or dA: the fused kernels recompute the bases -- kan.hip.)
 struct KanWs {
-  float* A[SIREN_KAN_MAX_LAYERS];
   float* X[SIREN_KAN_MAX_LAYERS + 1];
   float* W[SIREN_KAN_MAX_LAYERS];
-  float *dW, *slab, *dA, *G[2], *sse_part, *gsum_part, *gmax_part, *zero;
+  float *dW, *slab, *G[2], *sse_part, *gsum_part, *gmax_part, *zero;
   int64_t total;
 };
 
@@ -666,7 +666,6 @@ KanWs kan_layout(const siren_kan_net* n, int64_t rows, int splits, float* base) 
   };
   int64_t wmax = 1, wk = 1;
   for (int l = 0; l < n->n_layers; ++l) {
-    w.A[l] = take(rows * KAN_K1 * n->width[l]);
     w.W[l] = take((int64_t)n->width[l + 1] * KAN_K1 * n->width[l]);
     const int64_t kw = (int64_t)n->width[l + 1] * KAN_K1 * n->width[l];
     if (kw > wk) wk = kw;
@@ -674,8 +673,12 @@ KanWs kan_layout(const siren_kan_net* n, int64_t rows, int splits, float* base) 
   }
   for (int l = 1; l <= n->n_layers; ++l) w.X[l] = take(rows * n->width[l]);
   w.dW = take(wk);
-  w.slab = take(wk * splits);
-  w.dA = take(rows * KAN_K1 * wmax);
+  // split-K slabs: splits x (out x 9 in) for the fused weight gradient, 4 splits x 9 in for the
+  // last layer's wave partials
+  int64_t slab = wk * splits;
+  for (int l = 0; l < n->n_layers; ++l)
+    if (n->width[l + 1] == 1 && 4LL * splits * KAN_K1 * n->width[l] > slab) slab = 4LL * splits * KAN_K1 * n->width[l];
+  w.slab = take(slab);
   w.G[0] = take(rows * wmax);
   w.G[1] = take(rows * wmax);
   const int64_t np = (rows + 255) / 256;
@@ -692,12 +695,12 @@ hipError_t kan_run_forward(const siren_kan_net* n, const siren_kan_batch* b, con
   const float* x = b->coords;
   for (int l = 0; l < n->n_layers; ++l) {
     const int in = n->width[l], out = n->width[l + 1];
-    const int64_t K = (int64_t)KAN_K1 * in;
-    SIREN_PROF(SIREN_PROF_KAN_EXPAND, s, kan_expand(x, n->grid[l], R, in, w.A[l], s));
     SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_combine(n->base_w[l], n->spline_w[l], n->scaler[l], out, in, w.W[l], s));
-    // X[l+1][r][o] = sum_k A[r][k] W[o][k]
-    SIREN_PROF(SIREN_PROF_KAN_GEMM, s, kan_gemm(w.A[l], K, 1, w.W[l], 1, K, (int)R, out, K, 1, nullptr,
-                                                w.X[l + 1], s));
+    // X[l+1][r][o] = sum_k A[r][k] W[o][k], A = [SiLU(x) | bases(x)] recomputed in LDS
+    if (out == 1 && in <= 64)
+      SIREN_PROF(SIREN_PROF_KAN_FWD, s, kan_head_fwd(x, n->grid[l], w.W[l], R, in, w.X[l + 1], s));
+    else
+      SIREN_PROF(SIREN_PROF_KAN_FWD, s, kan_fwd_fused(x, n->grid[l], w.W[l], R, in, out, w.X[l + 1], s));
     x = w.X[l + 1];
   }
   return hipSuccess;
@@ -752,15 +755,24 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, si
   int cur = 0;
   for (int l = net->n_layers - 1; l >= 0; --l) {
     const int in = net->width[l], out = net->width[l + 1];
-    const int64_t K = (int64_t)KAN_K1 * in;
-    // dW[o][k] = sum_r G[r][o] A[r][k]  (split-K over the coordinates)
-    SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_gemm(G, 1, out, w.A[l], K, 1, out, (int)K, R, b->splits, w.slab, w.dW, s));
+    const float* xl = l == 0 ? b->coords : w.X[l];
+    if (out == 1 && in <= 64 && l > 0) {
+      // last layer: weight gradient and dX in one pass over the rows (rank-1 dA)
+      SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_head_bwd(xl, net->grid[l], w.W[l], G, R, in, 4 * b->splits, w.slab,
+                                                    w.dW, w.G[cur], s));
+      SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
+                                                         gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
+      G = w.G[cur];
+      cur ^= 1;
+      continue;
+    }
+    // dW[o][k] = sum_r G[r][o] A[r][k]  (split-K over the coordinates, bases recomputed)
+    SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_dw_fused(xl, net->grid[l], G, R, in, out, b->splits, w.slab, w.dW, s));
     SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
                                                        gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
     if (l == 0) break;
-    // dA[r][k] = sum_o G[r][o] W[o][k];  dX = SiLU' dA_base + sum_c B'_c dA_spline_c
-    SIREN_PROF(SIREN_PROF_KAN_DA, s, kan_gemm(G, out, 1, w.W[l], K, 1, (int)R, (int)K, out, 1, nullptr, w.dA, s));
-    SIREN_PROF(SIREN_PROF_KAN_CONTRACT, s, kan_contract(w.X[l], net->grid[l], w.dA, R, in, w.G[cur], s));
+    // dX = SiLU' dA_base + sum_c B'_c dA_spline_c with dA = G W formed per chunk in LDS
+    SIREN_PROF(SIREN_PROF_KAN_DX, s, kan_dx_fused(xl, net->grid[l], G, w.W[l], R, in, out, w.G[cur], s));
     G = w.G[cur];
     cur ^= 1;
   }

@@ -124,9 +124,19 @@ hipError_t fp32_linear_bwd(const float* x, int64_t rows, int in, int out, const 
                            float* gx, float* gW, float* gb, float* slab, int splits, float* tmp, hipStream_t s);
 
 // KAN (kan.hip): fp32, grid_size 5, spline_order 3 (9 A-columns per input)
-hipError_t kan_expand(const float* X, const float* grid, int64_t N, int in, float* A, hipStream_t s);
-hipError_t kan_contract(const float* X, const float* grid, const float* dA, int64_t N, int in, float* dX,
-                        hipStream_t s);
+// fused layer kernels (the bases are recomputed in LDS; A and dA never reach HBM)
+hipError_t kan_fwd_fused(const float* X, const float* grid, const float* W, int64_t N, int in, int out, float* Y,
+                         hipStream_t s);
+int64_t kan_dw_slab_floats(int in, int out, int splits);
+hipError_t kan_dw_fused(const float* X, const float* grid, const float* G, int64_t N, int in, int out, int splits,
+                        float* slab, float* dW, hipStream_t s);
+hipError_t kan_dx_fused(const float* X, const float* grid, const float* Gout, const float* W, int64_t N, int in,
+                        int out, float* Gin, hipStream_t s);
+// the last layer (out = 1, in <= 64): wave-per-row forward; backward with the weight-gradient
+// partials of `waves` (multiple of 4) row runs in `slab` and Gin, dA never formed
+hipError_t kan_head_fwd(const float* X, const float* grid, const float* W, int64_t N, int in, float* Y, hipStream_t s);
+hipError_t kan_head_bwd(const float* X, const float* grid, const float* W, const float* g, int64_t N, int in, int waves,
+                        float* slab, float* dW, float* Gin, hipStream_t s);
 hipError_t kan_combine(const float* base_w, const float* spline_w, const float* scaler, int out, int in, float* W,
                        hipStream_t s);
 hipError_t kan_param_grads(const float* dW, const float* spline_w, const float* scaler, int out, int in,

@@ -56,7 +56,7 @@ def test_torchrun_two_ranks_gloo():
 def test_kan_config():
     res = _run([sys.executable, "bench.py", "--config", "cfg5", "--steps", "2", "--warmup", "1", "--coords", "50000"])
     assert res["n_gpus"] == 1 and res["value"] > 0 and res["dtype"] == "fp32"
-    assert res["config"]["widths"] == [1, 64, 64, 1] and res["roofline"]["bound"] == "hbm"
+    assert res["config"]["widths"] == [1, 64, 64, 1] and res["roofline"]["bound"] == "mfma"
     assert 0 < res["roofline"]["frac"] < 1 and res["roofline"]["kernel"].startswith("kan_")
 
 
