@@ -643,15 +643,17 @@ int check_kan(const siren_kan_net* n) {
 }
 
 // Workspace carve-up (floats, each piece 64-float aligned):
-//   X[l] rows x w[l] for l = 1..L (X[L] = the output row vector);  W[l] w[l+1] x 9 w[l];
+//   X[l] rows x w[l] for l = 1..L (X[L] = the output row vector);  W[l] w[l+1] x 9 w[l] and its
+//   transpose WT[l];
 //   dW w_max_out x 9 w_max_in;  slab splits x that;  G[2] rows x w_max;
 //   sse/gsum/gmax partials 3 x ceil(rows/256);  one zero float.
 // (No expansion A or dA: the fused kernels recompute the bases -- kan.hip.)
 struct KanWs {
   float* X[SIREN_KAN_MAX_LAYERS + 1];
   float* W[SIREN_KAN_MAX_LAYERS];
+  float* WT[SIREN_KAN_MAX_LAYERS];  // W transposed, [9 in][out] (the dX kernel's operand)
   float *dW, *slab, *G[2], *sse_part, *gsum_part, *gmax_part, *zero;
-  int64_t total;
+  int64_t slab_floats, total;
 };
 
 inline int64_t al64(int64_t x) { return (x + 63) / 64 * 64; }
@@ -667,6 +669,7 @@ KanWs kan_layout(const siren_kan_net* n, int64_t rows, int splits, float* base) 
   int64_t wmax = 1, wk = 1;
   for (int l = 0; l < n->n_layers; ++l) {
     w.W[l] = take((int64_t)n->width[l + 1] * KAN_K1 * n->width[l]);
+    w.WT[l] = take((int64_t)n->width[l + 1] * KAN_K1 * n->width[l]);
     const int64_t kw = (int64_t)n->width[l + 1] * KAN_K1 * n->width[l];
     if (kw > wk) wk = kw;
     if (n->width[l] > wmax) wmax = n->width[l];
@@ -679,6 +682,7 @@ KanWs kan_layout(const siren_kan_net* n, int64_t rows, int splits, float* base) 
   for (int l = 0; l < n->n_layers; ++l)
     if (n->width[l + 1] == 1 && 4LL * splits * KAN_K1 * n->width[l] > slab) slab = 4LL * splits * KAN_K1 * n->width[l];
   w.slab = take(slab);
+  w.slab_floats = slab;
   w.G[0] = take(rows * wmax);
   w.G[1] = take(rows * wmax);
   const int64_t np = (rows + 255) / 256;
@@ -695,7 +699,7 @@ hipError_t kan_run_forward(const siren_kan_net* n, const siren_kan_batch* b, con
   const float* x = b->coords;
   for (int l = 0; l < n->n_layers; ++l) {
     const int in = n->width[l], out = n->width[l + 1];
-    SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_combine(n->base_w[l], n->spline_w[l], n->scaler[l], out, in, w.W[l], s));
+    SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_combine(n->base_w[l], n->spline_w[l], n->scaler[l], out, in, w.W[l], w.WT[l], s));
     // X[l+1][r][o] = sum_k A[r][k] W[o][k], A = [SiLU(x) | bases(x)] recomputed in LDS
     if (out == 1 && in <= 64)
       SIREN_PROF(SIREN_PROF_KAN_FWD, s, kan_head_fwd(x, n->grid[l], w.W[l], R, in, w.X[l + 1], s));
@@ -758,7 +762,7 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, si
     const float* xl = l == 0 ? b->coords : w.X[l];
     if (out == 1 && in <= 64 && l > 0) {
       // last layer: weight gradient and dX in one pass over the rows (rank-1 dA)
-      SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_head_bwd(xl, net->grid[l], w.W[l], G, R, in, 4 * b->splits, w.slab,
+      SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_head_bwd(xl, net->grid[l], w.W[l], G, R, in, w.slab_floats / (KAN_K1 * in), w.slab,
                                                     w.dW, w.G[cur], s));
       SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
                                                          gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
@@ -767,12 +771,13 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, si
       continue;
     }
     // dW[o][k] = sum_r G[r][o] A[r][k]  (split-K over the coordinates, bases recomputed)
-    SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_dw_fused(xl, net->grid[l], G, R, in, out, b->splits, w.slab, w.dW, s));
+    SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_dw_fused(xl, net->grid[l], G, R, in, out,
+                                                    w.slab_floats / ((int64_t)out * KAN_K1 * in), w.slab, w.dW, s));
     SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
                                                        gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
     if (l == 0) break;
     // dX = SiLU' dA_base + sum_c B'_c dA_spline_c with dA = G W formed per chunk in LDS
-    SIREN_PROF(SIREN_PROF_KAN_DX, s, kan_dx_fused(xl, net->grid[l], G, w.W[l], R, in, out, w.G[cur], s));
+    SIREN_PROF(SIREN_PROF_KAN_DX, s, kan_dx_fused(xl, net->grid[l], G, w.WT[l], R, in, out, w.G[cur], s));
     G = w.G[cur];
     cur ^= 1;
   }

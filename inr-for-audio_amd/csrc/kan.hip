@@ -5,17 +5,23 @@
 //
 // A and dA are never materialised (round 2; the first design wrote and re-read A / dA, 2.3 KB
 // per coordinate each at width 64, ~26 KB of HBM per coordinate-step).  Three fused kernels
-// recompute the bases of an (8-input x 64-row) chunk into LDS where they are consumed:
+// recompute the bases of a (16-input x 64-row) chunk into LDS where they are consumed:
 //   kan_fwd_fused  Out tile [64 rows][64 outs] = sum over input chunks of A_chunk W_chunk^T
-//   kan_dw_fused   dW chunk [out][72] += G[rows]^T A_chunk[rows]   (split-K over rows, slabs)
+//   kan_dw_fused   dW chunk [out][144] += G[rows]^T A_chunk[rows]   (split-K over rows, slabs)
 //   kan_dx_fused   dA_chunk = G W_chunk (in LDS), contracted at once with the bases' derivatives
 // Everything is fp32 like the reference.  The bases follow kan.py:94-104's Cox-de Boor
 // recursion op for op (sub, div, mul, add; fp-contract off) on the layer's own `grid` buffer,
 // so they are bit-identical to torch's CPU result; the derivative differentiates the same
-// recursion.  The GEMMs are short (K = 9 in <= 2304, out <= 256): LDS-tiled VALU FMAs, not MFMA
-// (SURVEY §8 f4).
+// recursion.  The chunk products run on the f32-input MFMA (exact f32); the last
+// layer (out = 1) is a per-row dot product on the VALU (kan_head_*).
 #include "siren_common.h"
 #include "siren_kernels.h"
+
+// KAN_ABL (measurement-only builds via tools/kan_ablate.py, never the product): bit 1 replaces
+// the basis recursion by a trivial stand-in, bit 2 skips the chunk products.
+#ifndef KAN_ABL
+#define KAN_ABL 0
+#endif
 
 namespace siren {
 
@@ -33,35 +39,52 @@ constexpr int KAN_K1 = 1 + KAN_NB;  // columns of A per input feature
 // non-zero; every other term of the full recursion is l*0 + r*0 = +-0 and, where it meets a
 // non-zero term, x + (+-0) = x.  Computing the window terms with the same operations in the
 // same order therefore gives the full recursion's values bit for bit (zeros up to sign), at 18
-// instead of 54 divisions (36 instead of 108 with the derivative).  The knots are read through
-// the pointer (a runtime-indexed register array would live in scratch).
-// RCP (backward kernels): the knot-difference divisions become products with reciprocals
-// inv[(k-1)*11 + j] = 1 / (g[j+k] - g[j]) precomputed per input (kf_fill_inv) -- within an ulp or
-// two of the divisions, which only the weight / input gradients see (the forward keeps the exact
-// divisions, so its bases stay bit-identical to torch's).
+// instead of 54 divisions (36 instead of 108 with the derivative).
+// The span search also captures the lane's knot window kw[d] = g[s-3+d] (d = 0..7) with selects,
+// so the recursion indexes registers statically: no per-lane knot gathers.  Terms whose knot
+// index falls outside the array are computed on stale window entries and discarded by a select
+// (the full recursion has no such term).
+// RCP (backward kernels): the knot-difference divisions become products with v_rcp_f32
+// reciprocals (within an ulp of the divisions; only the weight / input gradients see them -- the
+// forward keeps the exact divisions, so its bases stay bit-identical to torch's).
 template <bool DERIV, bool RCP = false>
-__device__ __forceinline__ void kan_bases_local(float x, const float* __restrict__ g, float* b, float* db,
-                                                const float* __restrict__ inv = nullptr) {
+__device__ __forceinline__ void kan_bases_local(float x, const float* __restrict__ g, float* b, float* db) {
+  float kn[KAN_NG];
+#pragma unroll
+  for (int j = 0; j < KAN_NG; ++j) kn[j] = g[j];
 #pragma unroll
   for (int j = 0; j < KAN_NB; ++j) b[j] = db[j] = 0.0f;
-  int s = -1;
+  if constexpr ((KAN_ABL & 1) != 0) {
 #pragma unroll
-  for (int j = 0; j < KAN_NG - 1; ++j)
-    if (x >= g[j] && x < g[j + 1]) s = j;
+    for (int j = 0; j < KAN_NB; ++j) b[j] = db[j] = x * kn[j];
+    return;
+  }
+  int s = -1;
+  float kw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < KAN_NG - 1; ++j) {
+    const bool hit = x >= kn[j] && x < kn[j + 1];
+    s = hit ? j : s;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const int t = j - 3 + d;
+      if (t >= 0 && t < KAN_NG) kw[d] = hit ? kn[t] : kw[d];
+    }
+  }
   if (s < 0) return;
   // window w[q] = B[s - 3 + q], q = 0..3, plus w[4] = B[s + 1] = 0
   float w[5] = {0.0f, 0.0f, 0.0f, 1.0f, 0.0f}, d[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int k = 1; k <= 3; ++k) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 3 - k; q < 4; ++q) {
       const int j = s - 3 + q;
-      if (q < 3 - k || j < 0 || j > KAN_NG - 2 - k) continue;  // outside the support / the array
-      const float gj = g[j], gjk = g[j + k], gj1 = g[j + 1], gjk1 = g[j + k + 1];
+      const bool ok = j >= 0 && j <= KAN_NG - 2 - k;  // inside the support and the array
+      const float gj = kw[q], gjk = kw[q + k], gj1 = kw[q + 1], gjk1 = kw[q + k + 1];
       float il, ir, l, r;
       if constexpr (RCP) {
-        il = inv[(k - 1) * 11 + j];
-        ir = inv[(k - 1) * 11 + j + 1];
+        il = __builtin_amdgcn_rcpf(gjk - gj);
+        ir = __builtin_amdgcn_rcpf(gjk1 - gj1);
         l = (x - gj) * il;
         r = (gjk1 - x) * ir;
       } else {
@@ -70,16 +93,22 @@ __device__ __forceinline__ void kan_bases_local(float x, const float* __restrict
         l = (x - gj) / (gjk - gj);
         r = (gjk1 - x) / (gjk1 - gj1);
       }
-      if constexpr (DERIV) d[q] = il * w[q] + l * d[q] - ir * w[q + 1] + r * d[q + 1];
-      w[q] = l * w[q] + r * w[q + 1];
+      if constexpr (DERIV) {
+        const float nd = il * w[q] + l * d[q] - ir * w[q + 1] + r * d[q + 1];
+        d[q] = ok ? nd : d[q];
+      }
+      const float nw = l * w[q] + r * w[q + 1];
+      w[q] = ok ? nw : w[q];
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int j = s - 3 + q;
-    if (j >= 0 && j < KAN_NB) {
-      b[j] = w[q];
-      if constexpr (DERIV) db[j] = d[q];
+  for (int c = 0; c < KAN_NB; ++c) {
+    // B[c] = w[c - s + 3] when that is a window slot
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool at = (c == s - 3 + q);
+      b[c] = at ? w[q] : b[c];
+      if constexpr (DERIV) db[c] = at ? d[q] : db[c];
     }
   }
 }
@@ -93,26 +122,65 @@ __device__ __forceinline__ float silu_grad(float x) {
 // ---- fused layer kernels --------------------------------------------------------------------
 // Chunk of IC inputs i0 .. i0+ic-1 (ic <= IC): local column kk < ic is the SiLU column of input
 // i0+kk (combined-weight column k = i0+kk), kk = ic + 8 ii + c the spline basis c of input i0+ii
-// (k = in + 8 (i0+ii) + c).
-constexpr int KF_IC = 8, KF_KC = 9 * KF_IC, KF_R = 64, KF_O = 64;
+// (k = in + 8 (i0+ii) + c).  kc = 9 ic columns, padded to kpad (a multiple of 16) with zeros.
+// The products run on v_mfma_f32_16x16x4_f32 (exact f32, a k-ordered fmaf chain; the same rate
+// as the f32 VALU but one LDS operand per 2048 flops instead of per 2): lane l supplies
+// A[l&15][k=l>>4] and B[k=l>>4][l&15]; D[row=(l>>4)*4+reg][col=l&15].
+constexpr int KF_IC = 16, KF_KC = 9 * KF_IC, KF_R = 64, KF_O = 64;
+constexpr int64_t kKanResidentBlocks = 512;  // 256 CUs x 2 (LDS-limited) for the fused kernels
 
 __device__ __forceinline__ int kf_col(int kk, int ic, int i0, int in) {
   return kk < ic ? i0 + kk : in + 8 * i0 + (kk - ic);
 }
 
-// As[kk][r] (r < 64 rows of the tile, pad 4) = A columns of the chunk for rows r0 + r; rows past N
-// are zero.  Every thread takes pairs (r, ii).
-template <bool RCP = false>
-__device__ __forceinline__ void kf_fill_a(float (*As)[KF_R + 4], const float* __restrict__ X,
-                                          const float* __restrict__ grid, int64_t N, int in, int64_t r0, int i0,
-                                          int ic, float (*inv)[33] = nullptr) {
-  for (int p = threadIdx.x; p < KF_R * ic; p += blockDim.x) {
-    const int r = p / ic, ii = p - r * ic;
+__device__ __forceinline__ f32x4 kf_mfma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Xs[r][ii] = X[r0 + r][i0 + ii] for rows < re (else 0): the chunk's inputs, read along the row
+// (a full chunk with in % 4 == 0: one 16-byte load per thread).  All tile loaders below issue
+// every load of the tile before the first LDS store, so a tile costs one memory latency.
+__device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+__device__ __forceinline__ void kf_stage_x(float (*Xs)[KF_IC + 1], const float* __restrict__ X, int64_t re, int in,
+                                           int64_t r0, int i0, int ic) {
+  if (ic == KF_IC && (in & 3) == 0) {
+    const int r = threadIdx.x >> 2, i4 = (threadIdx.x & 3) * 4;
+    float4 v = float4{0.f, 0.f, 0.f, 0.f};
+    if (r0 + r < re) v = ldg4(X + (r0 + r) * in + i0 + i4);
+    Xs[r][i4] = v.x;
+    Xs[r][i4 + 1] = v.y;
+    Xs[r][i4 + 2] = v.z;
+    Xs[r][i4 + 3] = v.w;
+    return;
+  }
+  for (int e = threadIdx.x; e < KF_R * KF_IC; e += blockDim.x) {
+    const int r = e / KF_IC, ii = e % KF_IC;
     const int64_t n = r0 + r;
+    Xs[r][ii] = (n < re && ii < ic) ? X[n * in + i0 + ii] : 0.f;
+  }
+}
+
+// gk[ii][j] = knot j of input i0 + ii.  The recursion reads knots at a per-row span index; from
+// LDS those reads cost an LDS round trip, from global memory an L1/L2 one on every step.
+constexpr int KF_GST = KAN_NG + 1;
+__device__ __forceinline__ void kf_fill_knots(float (*gk)[KF_GST], const float* __restrict__ grid, int i0, int ic) {
+  for (int e = threadIdx.x; e < ic * KAN_NG; e += blockDim.x) gk[e / KAN_NG][e % KAN_NG] = grid[i0 * KAN_NG + e];
+}
+
+// As[kk][r] (pad 4) = A columns of the chunk for rows r0 + r (zero past re, and rows kc .. kpad-1
+// zero).  A wave takes one input ii and 64 consecutive rows: its knots / reciprocals are uniform
+// and the LDS writes are conflict-free.
+template <bool RCP = false>
+__device__ __forceinline__ void kf_fill_a(float (*As)[KF_R + 4], const float (*Xs)[KF_IC + 1],
+                                          const float (*gk)[KF_GST], int64_t re, int64_t r0, int i0, int ic,
+                                          int kpad) {
+  for (int p = threadIdx.x; p < KF_R * ic; p += blockDim.x) {
+    const int r = p & (KF_R - 1), ii = p >> 6;
     float b[KAN_NB], unused[KAN_NB], sl = 0.f;
-    if (n < N) {
-      const float x = X[n * in + i0 + ii];
-      kan_bases_local<false, RCP>(x, grid + (i0 + ii) * KAN_NG, b, unused, RCP ? inv[ii] : nullptr);
+    if (r0 + r < re) {
+      const float x = Xs[r][ii];
+      kan_bases_local<false, RCP>(x, gk[ii], b, unused);
       sl = silu(x);
     } else {
 #pragma unroll
@@ -122,95 +190,196 @@ __device__ __forceinline__ void kf_fill_a(float (*As)[KF_R + 4], const float* __
 #pragma unroll
     for (int c = 0; c < KAN_NB; ++c) As[ic + 8 * ii + c][r] = b[c];
   }
+  const int kc = 9 * ic;
+  for (int e = threadIdx.x; e < (kpad - kc) * KF_R; e += blockDim.x) As[kc + e / KF_R][e % KF_R] = 0.f;
 }
 
-// Y[n][o] = sum_k A[n][k] W[o][k]; grid (ceil(N/64), ceil(out/64)); 4x4 outputs per thread.
+// Operand tiles are read with one ds_read_b128 per lane per 16-k group: lane group lk = l>>4
+// supplies k = 16 g + 4 lk + t to the t-th MFMA of group g (a permutation of the summation index
+// applied to both operands alike).  Row strides are 4 mod 32 floats, so each 8-lane phase of a
+// b128 read covers the 32 banks once.  The next group's fragments are loaded while the current
+// group's MFMAs issue.
+constexpr int KF_AST = KF_KC + 4;  // [row][kk] tiles of the forward
+constexpr int KF_CST = KF_R + 4;   // [*][row] / [*][o] tiles of the backward
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float f4(const float4& v, int t) { return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w; }
+
+// acc[j] += sum over ng groups of 16 k: A(16 rows at ap) x B(16 cols at bp + j * bstride)
+template <int NJ>
+__device__ __forceinline__ void kf_mfma_groups(const float* ap, const float* bp, int bstride, int ng, f32x4 (&acc)[9]) {
+  float4 a = ld4(ap), b[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) b[j] = ld4(bp + j * bstride);
+  for (int g = 0; g < ng; ++g) {
+    float4 an = a, bn[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bn[j] = b[j];
+    if (g + 1 < ng) {
+      an = ld4(ap + 16 * (g + 1));
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bn[j] = ld4(bp + j * bstride + 16 * (g + 1));
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[j] = kf_mfma(f4(a, t), f4(b[j], t), acc[j]);
+    a = an;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) b[j] = bn[j];
+  }
+}
+
+// the same with a run-time count of B column tiles (1 .. 9)
+__device__ __forceinline__ void kf_mfma_groups_n(int nj, const float* ap, const float* bp, int bstride, int ng,
+                                                 f32x4 (&acc)[9]) {
+  switch (nj) {
+    case 9: kf_mfma_groups<9>(ap, bp, bstride, ng, acc); break;
+    case 8: kf_mfma_groups<8>(ap, bp, bstride, ng, acc); break;
+    case 7: kf_mfma_groups<7>(ap, bp, bstride, ng, acc); break;
+    case 6: kf_mfma_groups<6>(ap, bp, bstride, ng, acc); break;
+    case 5: kf_mfma_groups<5>(ap, bp, bstride, ng, acc); break;
+    case 4: kf_mfma_groups<4>(ap, bp, bstride, ng, acc); break;
+    case 3: kf_mfma_groups<3>(ap, bp, bstride, ng, acc); break;
+    case 2: kf_mfma_groups<2>(ap, bp, bstride, ng, acc); break;
+    default: kf_mfma_groups<1>(ap, bp, bstride, ng, acc); break;
+  }
+}
+
+// As[r][kk] = A columns of the chunk for rows r0 + r (zero past re; columns kc .. kpad-1 zero).
+// A wave takes one input ii and 64 consecutive rows; the 8 bases go out as two b128 stores.
+__device__ __forceinline__ void kf_fill_a_rows(float (*As)[KF_AST], const float (*Xs)[KF_IC + 1],
+                                               const float (*gk)[KF_GST], int64_t re, int64_t r0, int ic, int kpad) {
+  for (int p = threadIdx.x; p < KF_R * ic; p += blockDim.x) {
+    const int r = p & (KF_R - 1), ii = p >> 6;
+    float b[KAN_NB], unused[KAN_NB], sl = 0.f;
+    if (r0 + r < re) {
+      const float x = Xs[r][ii];
+      kan_bases_local<false>(x, gk[ii], b, unused);
+      sl = silu(x);
+    } else {
+#pragma unroll
+      for (int c = 0; c < KAN_NB; ++c) b[c] = 0.f;
+    }
+    As[r][ii] = sl;
+    float* d = &As[r][ic + 8 * ii];
+    if ((ic & 3) == 0) {
+      *reinterpret_cast<float4*>(d) = float4{b[0], b[1], b[2], b[3]};
+      *reinterpret_cast<float4*>(d + 4) = float4{b[4], b[5], b[6], b[7]};
+    } else {
+#pragma unroll
+      for (int c = 0; c < KAN_NB; ++c) d[c] = b[c];
+    }
+  }
+  const int kc = 9 * ic;
+  for (int e = threadIdx.x; e < (kpad - kc) * KF_R; e += blockDim.x) As[e % KF_R][kc + e / KF_R] = 0.f;
+}
+
+// Y[n][o] = sum_k A[n][k] W[o][k]; grid (ceil(N/64), ceil(out/64)).  Wave w: rows 16w .. 16w+15
+// x 64 outs (4 accumulators), K = the chunk's kpad columns, summed over the chunks.
 __global__ __launch_bounds__(256) void kan_fwd_fused_kernel(const float* __restrict__ X, const float* __restrict__ grid,
                                                             const float* __restrict__ W, int64_t N, int in, int out,
                                                             float* __restrict__ Y) {
-  __shared__ __attribute__((aligned(16))) float As[KF_KC][KF_R + 4];
-  __shared__ __attribute__((aligned(16))) float Ws[KF_KC][KF_O + 4];
-  const int tid = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float As[KF_R][KF_AST];  // [row][kk]
+  __shared__ __attribute__((aligned(16))) float Ws[KF_O][KF_AST];  // [o][kk]
+  __shared__ float Xs[KF_R][KF_IC + 1];
+  __shared__ float gk[KF_IC][KF_GST];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lk = lane >> 4;
   const int64_t r0 = (int64_t)blockIdx.x * KF_R;
   const int o0 = blockIdx.y * KF_O;
-  const int tm = (tid >> 4) * 4, tn = (tid & 15) * 4;
   const int64_t K = (int64_t)KAN_K1 * in;
-  float acc[4][4] = {};
+  f32x4 acc[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int i0 = 0; i0 < in; i0 += KF_IC) {
-    const int ic = in - i0 < KF_IC ? in - i0 : KF_IC, kc = 9 * ic;
-    kf_fill_a(As, X, grid, N, in, r0, i0, ic);
-    for (int e = tid; e < KF_O * kc; e += blockDim.x) {
-      const int o = e / kc, kk = e - o * kc;
-      Ws[kk][o] = (o0 + o < out) ? W[(int64_t)(o0 + o) * K + kf_col(kk, ic, i0, in)] : 0.f;
+    const int ic = in - i0 < KF_IC ? in - i0 : KF_IC, kc = 9 * ic, kpad = (kc + 15) & ~15;
+    kf_stage_x(Xs, X, N, in, r0, i0, ic);
+    kf_fill_knots(gk, grid, i0, ic);
+    if (ic == KF_IC && (in & 3) == 0) {
+      // Ws[o][4 c4 ..] <- 16-byte pieces of W's rows: 4 SiLU + 32 spline pieces per out
+      float4 v[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        const int idx = tid + 256 * q, o = idx / 36, c4 = idx % 36;
+        const int64_t col = c4 < 4 ? i0 + 4 * c4 : in + 8 * i0 + 4 * (c4 - 4);
+        v[q] = o0 + o < out ? ldg4(W + (int64_t)(o0 + o) * K + col) : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        const int idx = tid + 256 * q, o = idx / 36, c4 = idx % 36;
+        *reinterpret_cast<float4*>(&Ws[o][4 * c4]) = v[q];
+      }
+    } else {
+      for (int e = tid; e < KF_O * kpad; e += blockDim.x) {
+        const int o = e / kpad, kk = e - o * kpad;
+        Ws[o][kk] = (o0 + o < out && kk < kc) ? W[(int64_t)(o0 + o) * K + kf_col(kk, ic, i0, in)] : 0.f;
+      }
     }
     __syncthreads();
-    for (int kk = 0; kk < kc; ++kk) {
-      const float4 a = *(const float4*)&As[kk][tm];
-      const float4 w = *(const float4*)&Ws[kk][tn];
-      const float av[4] = {a.x, a.y, a.z, a.w}, wv[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * wv[j];
-    }
+    kf_fill_a_rows(As, Xs, gk, N, r0, ic, kpad);
+    __syncthreads();
+    if ((KAN_ABL & 2) == 0)
+      kf_mfma_groups<4>(&As[16 * wv + li][4 * lk], &Ws[li][4 * lk], 16 * KF_AST, kpad >> 4, acc);
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t n = r0 + tm + i;
-      const int o = o0 + tn + j;
-      if (n < N && o < out) Y[n * out + o] = acc[i][j];
+    for (int q = 0; q < 4; ++q) {
+      const int64_t n = r0 + 16 * wv + 4 * lk + q;
+      const int o = o0 + 16 * j + li;
+      if (n < N && o < out) Y[n * out + o] = acc[j][q];
     }
 }
 
-// inv[ii][(k-1)*11 + j] = 1 / (g[j+k] - g[j]) for the knots of inputs i0 .. i0+ic-1 (RCP bases)
-__device__ __forceinline__ void kf_fill_inv(float (*inv)[33], const float* __restrict__ grid, int i0, int ic) {
-  for (int e = threadIdx.x; e < ic * 33; e += blockDim.x) {
-    const int ii = e / 33, q = e - ii * 33, k = q / 11 + 1, j = q - (k - 1) * 11;
-    const float* g = grid + (i0 + ii) * KAN_NG;
-    inv[ii][q] = (j + k < KAN_NG) ? 1.0f / (g[j + k] - g[j]) : 0.0f;
-  }
-}
-
-// ---- the last layer (out = 1): one wave per row, lane = input (strided by 64) -------------
-// out[n] = sum_i SiLU(x_i) W[i] + sum_c B_c(x_i) W[in + 8 i + c], a fixed-order wave sum.
+// ---- the last layer (out = 1, in <= 64): one wave per row, lane = input ----------------------
+// out[n] = SiLU(x_lane) W[lane] + sum_c B_c(x_lane) W[in + 8 lane + c], summed over the wave in a
+// fixed butterfly order.
 __global__ __launch_bounds__(256) void kan_head_fwd_kernel(const float* __restrict__ X, const float* __restrict__ grid,
                                                            const float* __restrict__ W, int64_t N, int in,
                                                            float* __restrict__ Y) {
+  __shared__ float gk[64][KF_GST];
+  kf_fill_knots(gk, grid, 0, in);
+  __syncthreads();
   const int lane = threadIdx.x & 63;
+  const bool on = lane < in;
+  float wb = 0.f, ws[KAN_NB] = {};
+  if (on) {
+    wb = W[lane];
+#pragma unroll
+    for (int c = 0; c < KAN_NB; ++c) ws[c] = W[in + KAN_NB * lane + c];
+  }
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
   for (int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); n < N; n += nw) {
     float v = 0.f;
-    for (int i = lane; i < in; i += 64) {
-      const float x = X[n * in + i];
+    if (on) {
+      const float x = X[n * in + lane];
       float b[KAN_NB], unused[KAN_NB];
-      kan_bases_local<false>(x, grid + i * KAN_NG, b, unused);
-      v += silu(x) * W[i];
+      kan_bases_local<false>(x, gk[lane], b, unused);
+      v = silu(x) * wb;
 #pragma unroll
-      for (int c = 0; c < KAN_NB; ++c) v += b[c] * W[in + KAN_NB * i + c];
+      for (int c = 0; c < KAN_NB; ++c) v += b[c] * ws[c];
     }
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     if (lane == 0) Y[n] = v;
   }
 }
 
-// Backward of the last layer for dLoss/dout = g: weight-gradient partials of this wave's rows
-// (slab[wave][k], summed later in fixed order) and Gin[n][i] = g_n (SiLU'(x) W[i] + sum_c B'_c(x)
-// W[in + 8 i + c]) -- dA = g W is a rank-1 product, so it is never formed.  Each wave takes a
-// contiguous run of rows; lanes own inputs (in <= 64).
+// Backward of the last layer for dLoss/dout = g: Gin[n][i] = g_n (SiLU'(x) W[i] + sum_c B'_c(x)
+// W[in + 8 i + c]) -- dA = g W is a rank-1 product, so it is never formed -- and the weight
+// gradient's partial sums over the block's contiguous rows (its 4 waves take every 4th row, then
+// add up in a fixed order) in slab row blockIdx.x, summed later in fixed order.  Lanes own inputs.
 __global__ __launch_bounds__(256) void kan_head_bwd_kernel(const float* __restrict__ X, const float* __restrict__ grid,
                                                            const float* __restrict__ W, const float* __restrict__ g,
-                                                           int64_t N, int in, int64_t rows_per_wave,
+                                                           int64_t N, int in, int64_t rows_per_block,
                                                            float* __restrict__ slab, float* __restrict__ Gin) {
-  __shared__ float inv[64][33];
-  kf_fill_inv(inv, grid, 0, in);
+  __shared__ float gk[64][KF_GST];
+  __shared__ float part[4][KAN_K1][64];
+  kf_fill_knots(gk, grid, 0, in);
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int64_t nb = wv * rows_per_wave;
-  const int64_t ne = nb + rows_per_wave < N ? nb + rows_per_wave : N;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nb = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t ne = nb + rows_per_block < N ? nb + rows_per_block : N;
   const bool on = lane < in;
   float wb = 0.f, ws[KAN_NB] = {};
   if (on) {
@@ -219,151 +388,223 @@ __global__ __launch_bounds__(256) void kan_head_bwd_kernel(const float* __restri
     for (int c = 0; c < KAN_NB; ++c) ws[c] = W[in + KAN_NB * lane + c];
   }
   float ab = 0.f, as[KAN_NB] = {};
-  for (int64_t n = nb; n < ne; ++n) {
-    if (!on) continue;
-    const float gn = g[n];
-    const float x = X[n * in + lane];
-    float b[KAN_NB], db[KAN_NB];
-    kan_bases_local<true, true>(x, grid + lane * KAN_NG, b, db, inv[lane]);
-    ab += gn * silu(x);
-    float v = silu_grad(x) * wb;
+  if (on)
+    for (int64_t n = nb + wv; n < ne; n += 4) {
+      const float gn = g[n];
+      const float x = X[n * in + lane];
+      float b[KAN_NB], db[KAN_NB];
+      kan_bases_local<true, true>(x, gk[lane], b, db);
+      ab += gn * silu(x);
+      float v = silu_grad(x) * wb;
 #pragma unroll
-    for (int c = 0; c < KAN_NB; ++c) {
-      as[c] += gn * b[c];
-      v += db[c] * ws[c];
+      for (int c = 0; c < KAN_NB; ++c) {
+        as[c] += gn * b[c];
+        v += db[c] * ws[c];
+      }
+      Gin[n * in + lane] = gn * v;
     }
-    Gin[n * in + lane] = gn * v;
-  }
-  if (on) {
-    float* row = slab + wv * (int64_t)KAN_K1 * in;
-    row[lane] = ab;
+  part[wv][0][lane] = ab;
 #pragma unroll
-    for (int c = 0; c < KAN_NB; ++c) row[in + KAN_NB * lane + c] = as[c];
+  for (int c = 0; c < KAN_NB; ++c) part[wv][1 + c][lane] = as[c];
+  __syncthreads();
+  if (wv == 0 && on) {
+    float* row = slab + (int64_t)blockIdx.x * KAN_K1 * in;
+#pragma unroll
+    for (int t = 0; t < KAN_K1; ++t) {
+      const float v = ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane];
+      row[t == 0 ? lane : in + KAN_NB * lane + (t - 1)] = v;
+    }
   }
 }
 
-// slab[z][o][k] = sum over rows of split z of G[n][o] A[n][k], for the chunk's columns k;
-// grid (ceil(in/IC), ceil(out/64), splits).  Thread: 2 outputs x 9 chunk columns.
+// slab[z][o][k] = sum over rows of split z of G[n][o] A[n][k], for the chunk's columns k.
+// 1-D grid of nchunk * nout * zpad blocks (zpad = splits rounded up to 8), numbered so that the
+// blocks of one split (which read the same rows of G and X) share an XCD: block L runs on XCD
+// L % 8.  Wave w: outs 16w .. 16w+15 x the chunk's kpad columns (kpad/16 accumulators), K = rows.
 __global__ __launch_bounds__(256) void kan_dw_fused_kernel(const float* __restrict__ X, const float* __restrict__ grid,
                                                            const float* __restrict__ G, int64_t N, int in, int out,
-                                                           int64_t rows_per_split, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float As[KF_KC][KF_R + 4];
-  __shared__ __attribute__((aligned(16))) float Gs[KF_R][KF_O + 4];
-  __shared__ float inv[KF_IC][33];
-  const int tid = threadIdx.x;
-  const int i0 = blockIdx.x * KF_IC, o0 = blockIdx.y * KF_O;
-  const int ic = in - i0 < KF_IC ? in - i0 : KF_IC, kc = 9 * ic;
-  kf_fill_inv(inv, grid, i0, ic);
-  __syncthreads();
-  const int64_t rb = (int64_t)blockIdx.z * rows_per_split;
+                                                           int64_t rows_per_split, int nchunk, int nout, int splits,
+                                                           float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float As[KF_KC][KF_CST];  // [kk][r]
+  __shared__ __attribute__((aligned(16))) float Gt[KF_O][KF_CST];   // [o][r]
+  __shared__ float Xs[KF_R][KF_IC + 1];
+  __shared__ float gk[KF_IC][KF_GST];
+  const int per = nchunk * nout, L = blockIdx.x, q8 = L >> 3;
+  const int cid = q8 % per, z = (q8 / per) * 8 + (L & 7);
+  if (z >= splits) return;  // whole block, before any barrier
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lk = lane >> 4;
+  const int i0 = (cid % nchunk) * KF_IC, o0 = (cid / nchunk) * KF_O;
+  const int ic = in - i0 < KF_IC ? in - i0 : KF_IC, kc = 9 * ic, kpad = (kc + 15) & ~15, nkt = kpad >> 4;
+  kf_fill_knots(gk, grid, i0, ic);
+  const int64_t rb = (int64_t)z * rows_per_split;
   const int64_t re = rb + rows_per_split < N ? rb + rows_per_split : N;
-  const int og = (tid & 31) * 2, kg = (tid >> 5) * 9;  // outs og, og+1; chunk columns kg .. kg+8
-  float acc[2][9] = {};
-  for (int64_t r0 = rb; r0 < re; r0 += KF_R) {
-    kf_fill_a<true>(As, X, grid, re, in, r0, i0, ic, inv);
-    for (int e = tid; e < KF_R * KF_O; e += blockDim.x) {
-      const int r = e / KF_O, o = e - r * KF_O;
-      Gs[r][o] = (r0 + r < re && o0 + o < out) ? G[(r0 + r) * out + o0 + o] : 0.f;
-    }
-    __syncthreads();
-    if (kg < kc) {
-      for (int r = 0; r < KF_R; ++r) {
-        const float2 g = *(const float2*)&Gs[r][og];
+  f32x4 acc[9];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) {
-          const float a = As[kg + j][r];
-          acc[0][j] += g.x * a;
-          acc[1][j] += g.y * a;
-        }
+  for (int j = 0; j < 9; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t r0 = rb; r0 < re; r0 += KF_R) {
+    kf_stage_x(Xs, X, re, in, r0, i0, ic);
+    if ((out & 3) == 0 && o0 + KF_O <= out) {
+      // lanes take consecutive rows (conflict-free transposed stores), 16 bytes of outs each
+      float4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int idx = tid + 256 * q, o4 = idx >> 6, r = idx & 63;
+        v[q] = r0 + r < re ? ldg4(G + (r0 + r) * out + o0 + 4 * o4) : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int idx = tid + 256 * q, o4 = idx >> 6, r = idx & 63;
+        Gt[4 * o4][r] = v[q].x;
+        Gt[4 * o4 + 1][r] = v[q].y;
+        Gt[4 * o4 + 2][r] = v[q].z;
+        Gt[4 * o4 + 3][r] = v[q].w;
+      }
+    } else {
+      for (int e = tid; e < KF_R * KF_O; e += blockDim.x) {
+        const int r = e / KF_O, o = e % KF_O;
+        Gt[o][r] = (r0 + r < re && o0 + o < out) ? G[(r0 + r) * out + o0 + o] : 0.f;
       }
     }
     __syncthreads();
+    kf_fill_a<true>(As, Xs, gk, re, r0, i0, ic, kpad);
+    __syncthreads();
+    if ((KAN_ABL & 2) == 0)
+      kf_mfma_groups_n(nkt, &Gt[16 * wv + li][4 * lk], &As[li][4 * lk], 16 * KF_CST, KF_R / 16, acc);
+    __syncthreads();
   }
   const int64_t K = (int64_t)KAN_K1 * in;
-  float* out_slab = slab + (int64_t)blockIdx.z * out * K;
+  float* out_slab = slab + (int64_t)z * out * K;
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int j = 0; j < 9; ++j) {
+    const int kk = 16 * j + li;
+    if (j >= nkt || kk >= kc) continue;
+    const int64_t col = kf_col(kk, ic, i0, in);
 #pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int o = o0 + og + h, kk = kg + j;
-      if (o < out && kk < kc) out_slab[(int64_t)o * K + kf_col(kk, ic, i0, in)] = acc[h][j];
+    for (int q = 0; q < 4; ++q) {
+      const int o = o0 + 16 * wv + 4 * lk + q;
+      if (o < out) out_slab[(int64_t)o * K + col] = acc[j][q];
     }
+  }
 }
 
-// Gin[n][i] = SiLU'(x) dA[n][i] + sum_c B'_c(x) dA[n][in + 8 i + c], dA = Gout W (never stored);
-// grid (ceil(N/64), ceil(in/IC)).  dA chunk: thread = 2 rows x 9 chunk columns, over out in chunks
-// of 64.
+// Gin[n][i] = SiLU'(x) dA[n][i] + sum_c B'_c(x) dA[n][in + 8 i + c], dA = Gout W (never stored;
+// W is read through its transposed copy WT[k][o], written by kan_combine);
+// grid ceil(N/64): a block takes 64 rows through every input chunk (its Gout rows stay in LDS
+// when out <= 64).  Wave w: rows 16w .. 16w+15 x the chunk's columns (kpad/16 accumulators),
+// K = outs; the dA tile then goes to LDS (over the W chunk) for the contraction with the bases'
+// derivatives, whose results leave through the X tile as coalesced row segments.
+constexpr int KF_DST = KF_KC + 1;  // dA row stride
+
 __global__ __launch_bounds__(256) void kan_dx_fused_kernel(const float* __restrict__ X, const float* __restrict__ grid,
-                                                           const float* __restrict__ Gout, const float* __restrict__ W,
+                                                           const float* __restrict__ Gout, const float* __restrict__ WT,
                                                            int64_t N, int in, int out, float* __restrict__ Gin) {
-  __shared__ __attribute__((aligned(16))) float Gs[KF_O][KF_R + 4];   // [o][r]
-  __shared__ __attribute__((aligned(16))) float Ws[KF_O][KF_KC + 4];  // [o][kk]
-  __shared__ __attribute__((aligned(16))) float dAs[KF_R][KF_KC + 1];
-  __shared__ float inv[KF_IC][33];
-  const int tid = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float Gs[KF_R][KF_CST];   // [r][o]
+  __shared__ __attribute__((aligned(16))) float WD[KF_KC * KF_CST];  // Wt[kk][o], then dAs[r][kk]
+  __shared__ float Xs[KF_R][KF_IC + 1];
+  __shared__ float gk[KF_IC][KF_GST];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lk = lane >> 4;
   const int64_t r0 = (int64_t)blockIdx.x * KF_R;
-  const int i0 = blockIdx.y * KF_IC;
-  const int ic = in - i0 < KF_IC ? in - i0 : KF_IC, kc = 9 * ic;
-  kf_fill_inv(inv, grid, i0, ic);
   const int64_t K = (int64_t)KAN_K1 * in;
-  const int rg = (tid & 31) * 2, kg = (tid >> 5) * 9;  // rows rg, rg+1; chunk columns kg .. kg+8
-  float acc[2][9] = {};
-  for (int oc = 0; oc < out; oc += KF_O) {
-    const int on = out - oc < KF_O ? out - oc : KF_O;
-    for (int e = tid; e < KF_R * on; e += blockDim.x) {
-      const int r = e / on, o = e - r * on;
-      Gs[o][r] = (r0 + r < N) ? Gout[(r0 + r) * out + oc + o] : 0.f;
-    }
-    for (int e = tid; e < on * kc; e += blockDim.x) {
-      const int o = e / kc, kk = e - o * kc;
-      Ws[o][kk] = W[(int64_t)(oc + o) * K + kf_col(kk, ic, i0, in)];
-    }
-    __syncthreads();
-    if (kg < kc) {
-      for (int o = 0; o < on; ++o) {
-        const float2 g = *(const float2*)&Gs[o][rg];
+  const bool g_once = out <= KF_O;
+  for (int i0 = 0; i0 < in; i0 += KF_IC) {
+    const int ic = in - i0 < KF_IC ? in - i0 : KF_IC, kc = 9 * ic, nkt = (kc + 15) >> 4;
+    f32x4 acc[9];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) {
-          const float w = Ws[o][kg + j];
-          acc[0][j] += g.x * w;
-          acc[1][j] += g.y * w;
+    for (int j = 0; j < 9; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    kf_fill_knots(gk, grid, i0, ic);
+    kf_stage_x(Xs, X, N, in, r0, i0, ic);
+    for (int oc = 0; oc < out; oc += KF_O) {
+      const int on = out - oc < KF_O ? out - oc : KF_O, opad = (on + 15) & ~15;
+      const bool vec = (out & 3) == 0 && on == KF_O;
+      if (!g_once || i0 == 0) {
+        if (vec) {
+          float4 v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int idx = tid + 256 * q, r = idx >> 4, o4 = idx & 15;
+            v[q] = r0 + r < N ? ldg4(Gout + (r0 + r) * out + oc + 4 * o4) : float4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int idx = tid + 256 * q, r = idx >> 4, o4 = idx & 15;
+            *reinterpret_cast<float4*>(&Gs[r][4 * o4]) = v[q];
+          }
+        } else {
+          for (int e = tid; e < KF_R * KF_O; e += blockDim.x) {
+            const int r = e / KF_O, o = e % KF_O;
+            Gs[r][o] = (r0 + r < N && o < on) ? Gout[(r0 + r) * out + oc + o] : 0.f;
+          }
         }
       }
+      // Wt[kk][o] = W[oc + o][col(kk)] from the transposed copy (rows along o: coalesced, no conflicts)
+      if (vec && ic == KF_IC && (in & 3) == 0) {
+        float4 v[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+          const int idx = tid + 256 * q, kk = idx >> 4, o4 = idx & 15;
+          v[q] = ldg4(WT + (int64_t)kf_col(kk, ic, i0, in) * out + oc + 4 * o4);
+        }
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+          const int idx = tid + 256 * q, kk = idx >> 4, o4 = idx & 15;
+          *reinterpret_cast<float4*>(&WD[kk * KF_CST + 4 * o4]) = v[q];
+        }
+      } else {
+        for (int e = tid; e < kc * KF_O; e += blockDim.x) {
+          const int kk = e / KF_O, o = e % KF_O;
+          WD[kk * KF_CST + o] = o < on ? WT[(int64_t)kf_col(kk, ic, i0, in) * out + oc + o] : 0.f;
+        }
+      }
+      __syncthreads();
+      if ((KAN_ABL & 2) == 0)
+        kf_mfma_groups_n(nkt, &Gs[16 * wv + li][4 * lk], &WD[li * KF_CST + 4 * lk], 16 * KF_CST, opad >> 4, acc);
+      __syncthreads();
+    }
+    // columns kc .. 16 nkt - 1 of dA hold products with stale LDS: never read below
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+      if (j < nkt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) WD[(16 * wv + 4 * lk + q) * KF_DST + 16 * j + li] = acc[j][q];
+    __syncthreads();
+    for (int p = tid; p < KF_R * ic; p += blockDim.x) {
+      const int r = p & (KF_R - 1), ii = p >> 6;
+      if (r0 + r >= N) continue;
+      const float x = Xs[r][ii];
+      float b[KAN_NB], db[KAN_NB];
+      kan_bases_local<true, true>(x, gk[ii], b, db);
+      const float* dA = WD + r * KF_DST;
+      float v = silu_grad(x) * dA[ii];
+#pragma unroll
+      for (int c = 0; c < KAN_NB; ++c) v += db[c] * dA[ic + 8 * ii + c];
+      Xs[r][ii] = v;  // same element this thread read: no barrier needed before the write
     }
     __syncthreads();
-  }
-  if (kg < kc) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int j = 0; j < 9; ++j) dAs[rg + h][kg + j] = acc[h][j];
-  }
-  __syncthreads();
-  for (int p = tid; p < KF_R * ic; p += blockDim.x) {
-    const int r = p / ic, ii = p - r * ic;
-    const int64_t n = r0 + r;
-    if (n >= N) continue;
-    const float x = X[n * in + i0 + ii];
-    float b[KAN_NB], db[KAN_NB];
-    kan_bases_local<true, true>(x, grid + (i0 + ii) * KAN_NG, b, db, inv[ii]);
-    float v = silu_grad(x) * dAs[r][ii];
-#pragma unroll
-    for (int c = 0; c < KAN_NB; ++c) v += db[c] * dAs[r][ic + 8 * ii + c];
-    Gin[n * in + i0 + ii] = v;
+    for (int e = tid; e < KF_R * ic; e += blockDim.x) {
+      const int r = e / ic, ii = e - r * ic;
+      if (r0 + r < N) Gin[(r0 + r) * in + i0 + ii] = Xs[r][ii];
+    }
+    __syncthreads();  // Xs / gk / WD are refilled by the next chunk
   }
 }
 
 // W[o][i] = base_w[o][i];  W[o][in + 8 i + c] = spline_w[o][i][c] * scaler[o][i]  (kan.py:145-151)
 __global__ void kan_combine_kernel(const float* __restrict__ base_w, const float* __restrict__ spline_w,
-                                   const float* __restrict__ scaler, int out, int in, float* __restrict__ W) {
+                                   const float* __restrict__ scaler, int out, int in, float* __restrict__ W,
+                                   float* __restrict__ WT) {
   const int total = out * in;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int o = e / in, i = e - o * in;
     float* row = W + (int64_t)o * KAN_K1 * in;
     row[i] = base_w[e];
+    if (WT) WT[(int64_t)i * out + o] = base_w[e];
     const float s = scaler[e];
 #pragma unroll
-    for (int c = 0; c < KAN_NB; ++c) row[in + KAN_NB * i + c] = spline_w[(int64_t)e * KAN_NB + c] * s;
+    for (int c = 0; c < KAN_NB; ++c) {
+      const float v = spline_w[(int64_t)e * KAN_NB + c] * s;
+      row[in + KAN_NB * i + c] = v;
+      if (WT) WT[(int64_t)(in + KAN_NB * i + c) * out + o] = v;
+    }
   }
 }
 
@@ -452,13 +693,43 @@ __global__ __launch_bounds__(256) void kan_gemm_kernel(const float* __restrict__
     }
 }
 
-__global__ void kan_slab_reduce_kernel(const float* __restrict__ slab, int splits, int64_t mn,
-                                       float* __restrict__ out) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < mn; e += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += slab[z * mn + e];
-    out[e] = s;
+// out[e] = sum_z slab[z][e] in a fixed order: a block takes C columns; its 256 / C thread groups
+// sum every (256/C)-th slab row (4 loads in flight per thread), then the group partials add up
+// in group order.  C = 64 for wide slabs; C = 16 (64-byte row segments, 16 groups) when there are
+// few columns and many slab rows.
+template <int C>
+__global__ __launch_bounds__(256) void kan_slab_reduce_kernel(const float* __restrict__ slab, int splits, int64_t mn,
+                                                              float* __restrict__ out) {
+  constexpr int NG = 256 / C;
+  __shared__ float part[NG][C];
+  const int col = threadIdx.x % C, grp = threadIdx.x / C;
+  const int64_t e = (int64_t)blockIdx.x * C + col;
+  float acc = 0.f;
+  if (e < mn) {
+    int z = grp;
+    for (; z + 3 * NG < splits; z += 4 * NG) {
+      const float a0 = slab[(int64_t)z * mn + e], a1 = slab[(int64_t)(z + NG) * mn + e];
+      const float a2 = slab[(int64_t)(z + 2 * NG) * mn + e], a3 = slab[(int64_t)(z + 3 * NG) * mn + e];
+      acc = (((acc + a0) + a1) + a2) + a3;
+    }
+    for (; z < splits; z += NG) acc += slab[(int64_t)z * mn + e];
   }
+  part[grp][col] = acc;
+  __syncthreads();
+  if (grp == 0 && e < mn) {
+    float v = part[0][col];
+#pragma unroll
+    for (int g = 1; g < NG; ++g) v += part[g][col];
+    out[e] = v;
+  }
+}
+
+static hipError_t slab_reduce(const float* slab, int splits, int64_t mn, float* out, hipStream_t s) {
+  if (mn < 64 * 256 && splits > 64)
+    hipLaunchKernelGGL(kan_slab_reduce_kernel<16>, dim3((unsigned)((mn + 15) / 16)), dim3(256), 0, s, slab, splits, mn, out);
+  else
+    hipLaunchKernelGGL(kan_slab_reduce_kernel<64>, dim3((unsigned)((mn + 63) / 64)), dim3(256), 0, s, slab, splits, mn, out);
+  return hipGetLastError();
 }
 
 static inline int ew_grid(int64_t n) {
@@ -477,53 +748,60 @@ hipError_t kan_fwd_fused(const float* X, const float* grid, const float* W, int6
 int64_t kan_dw_slab_floats(int in, int out, int splits) { return (int64_t)splits * out * KAN_K1 * in; }
 
 hipError_t kan_head_fwd(const float* X, const float* grid, const float* W, int64_t N, int in, float* Y, hipStream_t s) {
-  if (N <= 0 || in <= 0) return hipErrorInvalidValue;
+  if (N <= 0 || in <= 0 || in > 64) return hipErrorInvalidValue;
   const int64_t blocks = (N + 3) / 4;
   hipLaunchKernelGGL(kan_head_fwd_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, X, grid, W,
                      N, in, Y);
   return hipGetLastError();
 }
 
-// out = 1 layer backward: `waves` waves of contiguous rows (waves <= slab rows), partial weight
-// gradients summed in fixed order into dW
-hipError_t kan_head_bwd(const float* X, const float* grid, const float* W, const float* g, int64_t N, int in, int waves,
-                        float* slab, float* dW, float* Gin, hipStream_t s) {
-  if (N <= 0 || in <= 0 || in > 64 || waves < 4) return hipErrorInvalidValue;
-  const int blocks = waves / 4;
-  int64_t rpw = (N + (int64_t)blocks * 4 - 1) / ((int64_t)blocks * 4);
-  if (rpw < 1) rpw = 1;
-  hipLaunchKernelGGL(kan_head_bwd_kernel, dim3(blocks), dim3(256), 0, s, X, grid, W, g, N, in, rpw, slab, Gin);
+// out = 1 layer backward: blocks of >= 128 contiguous rows, one slab row each (at most `slots`),
+// partial weight gradients summed in fixed order into dW
+hipError_t kan_head_bwd(const float* X, const float* grid, const float* W, const float* g, int64_t N, int in,
+                        int64_t slots, float* slab, float* dW, float* Gin, hipStream_t s) {
+  if (N <= 0 || in <= 0 || in > 64 || slots < 1) return hipErrorInvalidValue;
+  int64_t blocks = (N + 127) / 128;
+  if (blocks > slots) blocks = slots;
+  if (blocks > 0x7fffffff) blocks = 0x7fffffff;
+  const int64_t rpb = (N + blocks - 1) / blocks;
+  blocks = (N + rpb - 1) / rpb;
+  hipLaunchKernelGGL(kan_head_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, grid, W, g, N, in, rpb, slab, Gin);
   const int64_t mn = (int64_t)KAN_K1 * in;
-  hipLaunchKernelGGL(kan_slab_reduce_kernel, dim3(ew_grid(mn)), dim3(256), 0, s, (const float*)slab, blocks * 4, mn, dW);
-  return hipGetLastError();
+  return slab_reduce(slab, (int)blocks, mn, dW, s);
 }
 
 // dW[o][k] = sum_n G[n][o] A[n][k]: `splits` row slices into slabs, then the fixed-order slab sum
-hipError_t kan_dw_fused(const float* X, const float* grid, const float* G, int64_t N, int in, int out, int splits,
-                        float* slab, float* dW, hipStream_t s) {
-  if (N <= 0 || in <= 0 || out <= 0 || splits < 1) return hipErrorInvalidValue;
+hipError_t kan_dw_fused(const float* X, const float* grid, const float* G, int64_t N, int in, int out,
+                        int64_t max_splits, float* slab, float* dW, hipStream_t s) {
+  if (N <= 0 || in <= 0 || out <= 0 || max_splits < 1) return hipErrorInvalidValue;
+  const int nchunk = (in + KF_IC - 1) / KF_IC, nout = (out + KF_O - 1) / KF_O;
+  // one round of resident blocks (2 per CU x 256 CUs): every CU busy, no tail
+  int64_t splits = kKanResidentBlocks / ((int64_t)nchunk * nout);
+  if (splits < 1) splits = 1;
+  if (splits > max_splits) splits = max_splits;
   int64_t rps = (N + splits - 1) / splits;
   rps = (rps + KF_R - 1) / KF_R * KF_R;
   const int z = (int)((N + rps - 1) / rps);
-  hipLaunchKernelGGL(kan_dw_fused_kernel, dim3((in + KF_IC - 1) / KF_IC, (out + KF_O - 1) / KF_O, z), dim3(256), 0, s,
-                     X, grid, G, N, in, out, rps, slab);
+  const int64_t blocks = (int64_t)nchunk * nout * ((z + 7) / 8 * 8);
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kan_dw_fused_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, grid, G, N, in, out, rps, nchunk,
+                     nout, z, slab);
   const int64_t mn = (int64_t)out * KAN_K1 * in;
-  hipLaunchKernelGGL(kan_slab_reduce_kernel, dim3(ew_grid(mn)), dim3(256), 0, s, (const float*)slab, z, mn, dW);
-  return hipGetLastError();
+  return slab_reduce(slab, z, mn, dW, s);
 }
 
-hipError_t kan_dx_fused(const float* X, const float* grid, const float* Gout, const float* W, int64_t N, int in,
+hipError_t kan_dx_fused(const float* X, const float* grid, const float* Gout, const float* WT, int64_t N, int in,
                         int out, float* Gin, hipStream_t s) {
   if (N <= 0 || in <= 0 || out <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kan_dx_fused_kernel, dim3((unsigned)((N + KF_R - 1) / KF_R), (in + KF_IC - 1) / KF_IC), dim3(256),
-                     0, s, X, grid, Gout, W, N, in, out, Gin);
+  hipLaunchKernelGGL(kan_dx_fused_kernel, dim3((unsigned)((N + KF_R - 1) / KF_R)), dim3(256), 0, s, X, grid, Gout, WT,
+                     N, in, out, Gin);
   return hipGetLastError();
 }
 
 hipError_t kan_combine(const float* base_w, const float* spline_w, const float* scaler, int out, int in, float* W,
-                       hipStream_t s) {
+                       float* WT, hipStream_t s) {
   hipLaunchKernelGGL(kan_combine_kernel, dim3(ew_grid((int64_t)out * in)), dim3(256), 0, s, base_w, spline_w,
-                     scaler, out, in, W);
+                     scaler, out, in, W, WT);
   return hipGetLastError();
 }
 
@@ -544,9 +822,7 @@ hipError_t kan_gemm(const float* A, int64_t sam, int64_t sak, const float* B, in
   dim3 grid((N + KG_T - 1) / KG_T, (M + KG_T - 1) / KG_T, z);
   hipLaunchKernelGGL(kan_gemm_kernel, grid, dim3(256), 0, s, A, sam, sak, B, sbk, sbn, z > 1 ? C : out, M, N, K,
                      kchunk);
-  if (z > 1)
-    hipLaunchKernelGGL(kan_slab_reduce_kernel, dim3(ew_grid((int64_t)M * N)), dim3(256), 0, s, C, z,
-                       (int64_t)M * N, out);
+  if (z > 1) return slab_reduce(C, z, (int64_t)M * N, out, s);
   return hipGetLastError();
 }
 

@@ -128,17 +128,19 @@ hipError_t fp32_linear_bwd(const float* x, int64_t rows, int in, int out, const 
 hipError_t kan_fwd_fused(const float* X, const float* grid, const float* W, int64_t N, int in, int out, float* Y,
                          hipStream_t s);
 int64_t kan_dw_slab_floats(int in, int out, int splits);
-hipError_t kan_dw_fused(const float* X, const float* grid, const float* G, int64_t N, int in, int out, int splits,
-                        float* slab, float* dW, hipStream_t s);
-hipError_t kan_dx_fused(const float* X, const float* grid, const float* Gout, const float* W, int64_t N, int in,
+// split-K over the rows: at most max_splits slabs of out x 9 in floats
+hipError_t kan_dw_fused(const float* X, const float* grid, const float* G, int64_t N, int in, int out,
+                        int64_t max_splits, float* slab, float* dW, hipStream_t s);
+hipError_t kan_dx_fused(const float* X, const float* grid, const float* Gout, const float* WT, int64_t N, int in,
                         int out, float* Gin, hipStream_t s);
 // the last layer (out = 1, in <= 64): wave-per-row forward; backward with the weight-gradient
-// partials of `waves` (multiple of 4) row runs in `slab` and Gin, dA never formed
+// partials of at most `slots` row runs (slab rows of 9 in floats) and Gin, dA never formed
 hipError_t kan_head_fwd(const float* X, const float* grid, const float* W, int64_t N, int in, float* Y, hipStream_t s);
-hipError_t kan_head_bwd(const float* X, const float* grid, const float* W, const float* g, int64_t N, int in, int waves,
-                        float* slab, float* dW, float* Gin, hipStream_t s);
+hipError_t kan_head_bwd(const float* X, const float* grid, const float* W, const float* g, int64_t N, int in,
+                        int64_t slots, float* slab, float* dW, float* Gin, hipStream_t s);
+// W = [base_w | spline_w * scaler] as [out][9 in], and (WT != null) its transpose [9 in][out]
 hipError_t kan_combine(const float* base_w, const float* spline_w, const float* scaler, int out, int in, float* W,
-                       hipStream_t s);
+                       float* WT, hipStream_t s);
 hipError_t kan_param_grads(const float* dW, const float* spline_w, const float* scaler, int out, int in,
                            int accumulate, float* g_base, float* g_spline, float* g_scaler, hipStream_t s);
 hipError_t kan_gemm(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn, int M,
