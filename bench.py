@@ -188,8 +188,10 @@ def run_kan(args, world, rank, dev, dist, lib, _lib):
         # compute-bound once the expansions stay on chip: the fp32 dense peak for the dtype
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": kernels[dom]["tflops"], "peak": PEAK_F32_TFLOPS,
                      "unit": "TFLOP/s", "frac": kernels[dom]["tflops"] / PEAK_F32_TFLOPS, "traffic": None,
-                     "peak_note": "fp32 dense (f32 MFMA = vector rate); the kernels issue fp32 VALU FMAs; "
-                                  "GEMM flops only (the B-spline recursion is extra VALU work)",
+                     "peak_note": "fp32 dense (f32 MFMA = vector rate); the chunk products run on "
+                                  "v_mfma_f32_16x16x4_f32, the out = 1 head on VALU FMAs; GEMM flops only "
+                                  "(the B-spline recursion, recomputed in each of the three passes, is extra "
+                                  "VALU work)",
                      "flops_per_row": fpr[dom], "rows_per_launch": rows,
                      "hbm": {"achieved": kernels[dom]["gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                              "frac": kernels[dom]["gbs"] / PEAK_HBM_GBS, "algorithmic_bytes_per_row": bpr[dom]}},
@@ -199,10 +201,45 @@ def run_kan(args, world, rank, dev, dist, lib, _lib):
         "kernels": kernels,
         "final_loss": eng.last_loss(),
     }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # A quarter of the SIREN sample (the B-spline expansion makes a CPU KAN step slow per
+        # coordinate), at the box's CPU share only: at os.cpu_count() = 256 threads the KAN step
+        # thrashes 40x (26 s a step, measured).
+        n_cpu = max(1024, args.cpu_coords // 4)
+        what = (f"torch-CPU fp32 port of run.py's KAN step (oracle/torch_cpu_step.py: efficient-KAN "
+                f"KANLinear, kan.py:6-166), KAN({widths}), {n_cpu} coords")
+        result["cpu_baseline"] = cpu_baseline_sweep(
+            lambda threads, steps: torch_cpu_kan(n_cpu, widths, steps, threads), args, what, share_only=True)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def torch_cpu_kan(n, widths, steps, threads):
+    from oracle import torch_cpu_step
+    return torch_cpu_step.kan_time_steps(n, tuple(widths), steps=steps, threads=threads)
+
+
+def cpu_baseline_sweep(fn, args, what, share_only=False):
+    """Time the CPU port at the box's CPU share and (unless share_only) at os.cpu_count() threads
+    (BASELINE.md CPU plan: median of steps 2..k); the faster is the reported value, the sweep is
+    kept beside it."""
+    cores = os.cpu_count() or 1
+    share = min(cores, int(os.environ.get("OMP_NUM_THREADS") or cores))
+    legs = [(share, args.cpu_steps)] + ([] if share_only else [(cores, max(3, args.cpu_steps // 2))])
+    sweep = {}
+    for threads, steps in legs:
+        if threads not in sweep:
+            sweep[threads] = fn(threads, steps)
+    best = sweep[max(sweep, key=lambda k: sweep[k]["coord_samples_per_sec"])]
+    return {"value": best["coord_samples_per_sec"], "unit": "coord-samples/s", "cores": best["threads"],
+            "kind": "port", "threads": best["threads"], "cpu_count": cores,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "threads_sweep": {str(k): {"value": v["coord_samples_per_sec"], "steps": v["steps"],
+                                       "step_s": [round(x, 3) for x in v["step_times"]]} for k, v in sweep.items()},
+            "sample": f"{what}, median of steps 2..k, best of torch.set_num_threads({sorted(sweep)}) "
+                      f"(os.cpu_count() = {cores}), {cpu_model()}"}
 
 
 def main():

@@ -70,3 +70,57 @@ def time_steps(n_coords=65536, hidden=1024, n_inner=4, steps=6, threads=None, om
     med = float(np.median(times[1:])) if len(times) > 1 else times[0]
     return {"sec_per_step": med, "coord_samples_per_sec": n_coords / med,
             "threads": torch.get_num_threads(), "n_coords": n_coords, "steps": steps, "step_times": times}
+
+
+class _KANLinear(nn.Module):
+    """efficient-KAN's KANLinear forward (kan.py:6-166; grid 5, order 3, SiLU base) in torch fp32."""
+
+    def __init__(self, fin, fout, grid_size=5, order=3, grid_range=(-1.0, 1.0)):
+        super().__init__()
+        self.order = order
+        h = (grid_range[1] - grid_range[0]) / grid_size
+        g = torch.arange(-order, grid_size + order + 1, dtype=torch.float32) * h + grid_range[0]
+        self.register_buffer("grid", g.expand(fin, -1).contiguous())
+        self.base_weight = nn.Parameter(torch.empty(fout, fin).uniform_(-1 / math.sqrt(fin), 1 / math.sqrt(fin)))
+        self.spline_weight = nn.Parameter(torch.randn(fout, fin, grid_size + order) * 0.1 / grid_size)
+        self.spline_scaler = nn.Parameter(torch.empty(fout, fin).uniform_(-1 / math.sqrt(fin), 1 / math.sqrt(fin)))
+
+    def b_splines(self, x):
+        g = self.grid
+        x = x.unsqueeze(-1)
+        b = ((x >= g[:, :-1]) & (x < g[:, 1:])).to(x.dtype)
+        for k in range(1, self.order + 1):
+            b = ((x - g[:, :-(k + 1)]) / (g[:, k:-1] - g[:, :-(k + 1)]) * b[:, :, :-1]
+                 + (g[:, k + 1:] - x) / (g[:, k + 1:] - g[:, 1:(-k)]) * b[:, :, 1:])
+        return b
+
+    def forward(self, x):
+        base = nn.functional.linear(nn.functional.silu(x), self.base_weight)
+        w = (self.spline_weight * self.spline_scaler.unsqueeze(-1)).view(self.spline_weight.shape[0], -1)
+        return base + nn.functional.linear(self.b_splines(x).view(x.shape[0], -1), w)
+
+
+def kan_time_steps(n_coords=65536, widths=(1, 64, 64, 1), steps=6, threads=None, seed=0):
+    """Median wall time of steps 2..k of the KAN full-batch loop (run.py:92-93, :156-187)."""
+    if threads:
+        torch.set_num_threads(int(threads))
+    torch.manual_seed(seed)
+    model = nn.Sequential(*[_KANLinear(a, b) for a, b in zip(widths[:-1], widths[1:])])
+    t = torch.linspace(-1, 1, n_coords).reshape(n_coords, 1)
+    y = 0.5 * torch.sin(37 * t) + 0.3 * torch.sin(91 * t + 0.5)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.8, patience=200, min_lr=1e-6)
+    mse = nn.MSELoss()
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        loss = mse(model(t), y)
+        _ = loss.item()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        sched.step(loss)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times[1:])) if len(times) > 1 else times[0]
+    return {"sec_per_step": med, "coord_samples_per_sec": n_coords / med,
+            "threads": torch.get_num_threads(), "n_coords": n_coords, "steps": steps, "step_times": times}
