@@ -105,21 +105,33 @@ PEAK_F32_TFLOPS = 157.3   # MI355X dense fp32 (f32-input MFMA = the vector rate;
 def kan_work_per_row(widths):
     """Algorithmic work per coordinate of one KAN training step, per launch kind, for the fused
     design (kan.hip): bytes (activations in and out; the expansions A / dA are recomputed in LDS,
-    never stored) and GEMM flops (2 x 9 in x out per layer and GEMM; the B-spline recursion's own
-    VALU work is not counted, so the flop fraction is a lower bound).  Per layer l (in -> out):
-      kan_fwd  reads X_l (4 in), writes X_{l+1} (4 out);           2*9*in*out flop
-      kan_dw   reads X_l and G_{l+1} (4 out);                       2*9*in*out flop
-      kan_dx   reads X_l, G_{l+1}, writes G_l (4 in)   (l > 0);     2*9*in*out flop
+    never stored) and GEMM flops (2 x 9 in x out per layer and product; the B-spline recursion's
+    own VALU work is not counted, so the flop fraction is a lower bound).  Per layer l (in -> out),
+    following siren_kan_train_step's dispatch:
+      kan_fwd  reads X_l (4 in), writes X_{l+1} (4 out);                           2*9*in*out flop
+      l = 0:                      kan_dw  reads X_0, G_1;                           2*9*in*out
+      l > 0, out = 1, in <= 64:   kan_dw  (head) reads X_l, g, writes G_l;          2 * 2*9*in
+      l > 0, out <= 64:           kan_dx  (dW + dX) reads X_l, G_{l+1}, writes G_l; 2 * 2*9*in*out
+      l > 0, out > 64:            kan_dw as l = 0, and kan_dx reads X_l, G_{l+1}, writes G_l
     Weights, slabs and partials are O(width^2) per launch, not per row, and left out."""
     by = {"kan_fwd": 0, "kan_dw": 0, "kan_dx": 0}
     fl = {"kan_fwd": 0, "kan_dw": 0, "kan_dx": 0}
     for l in range(len(widths) - 1):
         i, o = widths[l], widths[l + 1]
         by["kan_fwd"] += 4 * i + 4 * o
-        by["kan_dw"] += 4 * i + 4 * o
         fl["kan_fwd"] += 18 * i * o
-        fl["kan_dw"] += 18 * i * o
-        if l > 0:
+        if l == 0:
+            by["kan_dw"] += 4 * i + 4 * o
+            fl["kan_dw"] += 18 * i * o
+        elif o == 1 and i <= 64:
+            by["kan_dw"] += 4 * i + 4 + 4 * i
+            fl["kan_dw"] += 36 * i
+        elif o <= 64:
+            by["kan_dx"] += 4 * i + 4 * o + 4 * i
+            fl["kan_dx"] += 36 * i * o
+        else:
+            by["kan_dw"] += 4 * i + 4 * o
+            fl["kan_dw"] += 18 * i * o
             by["kan_dx"] += 4 * i + 4 * o + 4 * i
             fl["kan_dx"] += 18 * i * o
     return by, fl

@@ -770,6 +770,17 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, si
       cur ^= 1;
       continue;
     }
+    const int64_t max_splits = w.slab_floats / ((int64_t)out * KAN_K1 * in);
+    if (l > 0 && out <= 64) {
+      // dW and dX = SiLU' dA_base + sum_c B'_c dA_c in one pass (bases and G read once)
+      SIREN_PROF(SIREN_PROF_KAN_DX, s, kan_bwd_fused(xl, net->grid[l], G, w.WT[l], R, in, out, max_splits, w.slab,
+                                                     w.dW, w.G[cur], s));
+      SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
+                                                         gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
+      G = w.G[cur];
+      cur ^= 1;
+      continue;
+    }
     // dW[o][k] = sum_r G[r][o] A[r][k]  (split-K over the coordinates, bases recomputed)
     SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_dw_fused(xl, net->grid[l], G, R, in, out,
                                                     w.slab_floats / ((int64_t)out * KAN_K1 * in), w.slab, w.dW, s));

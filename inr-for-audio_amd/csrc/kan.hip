@@ -127,7 +127,8 @@ __device__ __forceinline__ float silu_grad(float x) {
 // as the f32 VALU but one LDS operand per 2048 flops instead of per 2): lane l supplies
 // A[l&15][k=l>>4] and B[k=l>>4][l&15]; D[row=(l>>4)*4+reg][col=l&15].
 constexpr int KF_IC = 16, KF_KC = 9 * KF_IC, KF_R = 64, KF_O = 64;
-constexpr int64_t kKanResidentBlocks = 512;  // 256 CUs x 2 (LDS-limited) for the fused kernels
+constexpr int64_t kKanResidentBlocks = 512;     // 256 CUs x 2 (LDS-limited) for the fused kernels
+constexpr int64_t kKanBwdResidentBlocks = 256;  // kan_bwd_fused: one 512-thread block per CU
 
 __device__ __forceinline__ int kf_col(int kk, int ic, int i0, int in) {
   return kk < ic ? i0 + kk : in + 8 * i0 + (kk - ic);
@@ -145,13 +146,15 @@ __device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cas
 __device__ __forceinline__ void kf_stage_x(float (*Xs)[KF_IC + 1], const float* __restrict__ X, int64_t re, int in,
                                            int64_t r0, int i0, int ic) {
   if (ic == KF_IC && (in & 3) == 0) {
-    const int r = threadIdx.x >> 2, i4 = (threadIdx.x & 3) * 4;
-    float4 v = float4{0.f, 0.f, 0.f, 0.f};
-    if (r0 + r < re) v = ldg4(X + (r0 + r) * in + i0 + i4);
-    Xs[r][i4] = v.x;
-    Xs[r][i4 + 1] = v.y;
-    Xs[r][i4 + 2] = v.z;
-    Xs[r][i4 + 3] = v.w;
+    if (threadIdx.x < KF_R * KF_IC / 4) {
+      const int r = threadIdx.x >> 2, i4 = (threadIdx.x & 3) * 4;
+      float4 v = float4{0.f, 0.f, 0.f, 0.f};
+      if (r0 + r < re) v = ldg4(X + (r0 + r) * in + i0 + i4);
+      Xs[r][i4] = v.x;
+      Xs[r][i4 + 1] = v.y;
+      Xs[r][i4 + 2] = v.z;
+      Xs[r][i4 + 3] = v.w;
+    }
     return;
   }
   for (int e = threadIdx.x; e < KF_R * KF_IC; e += blockDim.x) {
@@ -206,8 +209,9 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 __device__ __forceinline__ float f4(const float4& v, int t) { return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w; }
 
 // acc[j] += sum over ng groups of 16 k: A(16 rows at ap) x B(16 cols at bp + j * bstride)
-template <int NJ>
-__device__ __forceinline__ void kf_mfma_groups(const float* ap, const float* bp, int bstride, int ng, f32x4 (&acc)[9]) {
+template <int NJ, int NA>
+__device__ __forceinline__ void kf_mfma_groups(const float* ap, const float* bp, int bstride, int ng, f32x4 (&acc)[NA]) {
+  static_assert(NJ <= NA, "more column tiles than accumulators");
   float4 a = ld4(ap), b[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) b[j] = ld4(bp + j * bstride);
@@ -230,19 +234,18 @@ __device__ __forceinline__ void kf_mfma_groups(const float* ap, const float* bp,
   }
 }
 
-// the same with a run-time count of B column tiles (1 .. 9)
+// the same with a run-time count of B column tiles (0 .. NA)
+template <int NA>
 __device__ __forceinline__ void kf_mfma_groups_n(int nj, const float* ap, const float* bp, int bstride, int ng,
-                                                 f32x4 (&acc)[9]) {
+                                                 f32x4 (&acc)[NA]) {
   switch (nj) {
-    case 9: kf_mfma_groups<9>(ap, bp, bstride, ng, acc); break;
-    case 8: kf_mfma_groups<8>(ap, bp, bstride, ng, acc); break;
-    case 7: kf_mfma_groups<7>(ap, bp, bstride, ng, acc); break;
-    case 6: kf_mfma_groups<6>(ap, bp, bstride, ng, acc); break;
-    case 5: kf_mfma_groups<5>(ap, bp, bstride, ng, acc); break;
-    case 4: kf_mfma_groups<4>(ap, bp, bstride, ng, acc); break;
-    case 3: kf_mfma_groups<3>(ap, bp, bstride, ng, acc); break;
-    case 2: kf_mfma_groups<2>(ap, bp, bstride, ng, acc); break;
-    default: kf_mfma_groups<1>(ap, bp, bstride, ng, acc); break;
+#define KF_CASE(n)                                                      \
+  case n:                                                               \
+    if constexpr (n <= NA) kf_mfma_groups<n>(ap, bp, bstride, ng, acc); \
+    break;
+    KF_CASE(9) KF_CASE(8) KF_CASE(7) KF_CASE(6) KF_CASE(5) KF_CASE(4) KF_CASE(3) KF_CASE(2) KF_CASE(1)
+#undef KF_CASE
+    default: break;
   }
 }
 
@@ -288,28 +291,39 @@ __global__ __launch_bounds__(256) void kan_fwd_fused_kernel(const float* __restr
   const int64_t r0 = (int64_t)blockIdx.x * KF_R;
   const int o0 = blockIdx.y * KF_O;
   const int64_t K = (int64_t)KAN_K1 * in;
-  f32x4 acc[9];
+  const bool vec = (in & 3) == 0 && in % KF_IC == 0;  // every chunk full, 16-byte pieces
+  f32x4 acc[4];
 #pragma unroll
-  for (int j = 0; j < 9; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // vec path: a chunk's W pieces (4 SiLU + 32 spline 16-byte pieces per out) and X piece, loaded
+  // into registers one chunk ahead so their latency hides under the previous chunk's products
+  const int xr = tid >> 2, xi = (tid & 3) * 4;
+  float4 wv4[9], xv4 = float4{0.f, 0.f, 0.f, 0.f};
+  auto load_chunk = [&](int i0) {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const int idx = tid + 256 * q, o = idx / 36, c4 = idx % 36;
+      const int64_t col = c4 < 4 ? i0 + 4 * c4 : in + 8 * i0 + 4 * (c4 - 4);
+      wv4[q] = o0 + o < out ? ldg4(W + (int64_t)(o0 + o) * K + col) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+    xv4 = r0 + xr < N ? ldg4(X + (r0 + xr) * in + i0 + xi) : float4{0.f, 0.f, 0.f, 0.f};
+  };
+  if (vec) load_chunk(0);
   for (int i0 = 0; i0 < in; i0 += KF_IC) {
     const int ic = in - i0 < KF_IC ? in - i0 : KF_IC, kc = 9 * ic, kpad = (kc + 15) & ~15;
-    kf_stage_x(Xs, X, N, in, r0, i0, ic);
     kf_fill_knots(gk, grid, i0, ic);
-    if (ic == KF_IC && (in & 3) == 0) {
-      // Ws[o][4 c4 ..] <- 16-byte pieces of W's rows: 4 SiLU + 32 spline pieces per out
-      float4 v[9];
+    if (vec) {
 #pragma unroll
       for (int q = 0; q < 9; ++q) {
         const int idx = tid + 256 * q, o = idx / 36, c4 = idx % 36;
-        const int64_t col = c4 < 4 ? i0 + 4 * c4 : in + 8 * i0 + 4 * (c4 - 4);
-        v[q] = o0 + o < out ? ldg4(W + (int64_t)(o0 + o) * K + col) : float4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<float4*>(&Ws[o][4 * c4]) = wv4[q];
       }
-#pragma unroll
-      for (int q = 0; q < 9; ++q) {
-        const int idx = tid + 256 * q, o = idx / 36, c4 = idx % 36;
-        *reinterpret_cast<float4*>(&Ws[o][4 * c4]) = v[q];
-      }
+      Xs[xr][xi] = xv4.x;
+      Xs[xr][xi + 1] = xv4.y;
+      Xs[xr][xi + 2] = xv4.z;
+      Xs[xr][xi + 3] = xv4.w;
     } else {
+      kf_stage_x(Xs, X, N, in, r0, i0, ic);
       for (int e = tid; e < KF_O * kpad; e += blockDim.x) {
         const int o = e / kpad, kk = e - o * kpad;
         Ws[o][kk] = (o0 + o < out && kk < kc) ? W[(int64_t)(o0 + o) * K + kf_col(kk, ic, i0, in)] : 0.f;
@@ -318,6 +332,7 @@ __global__ __launch_bounds__(256) void kan_fwd_fused_kernel(const float* __restr
     __syncthreads();
     kf_fill_a_rows(As, Xs, gk, N, r0, ic, kpad);
     __syncthreads();
+    if (vec && i0 + KF_IC < in) load_chunk(i0 + KF_IC);
     if ((KAN_ABL & 2) == 0)
       kf_mfma_groups<4>(&As[16 * wv + li][4 * lk], &Ws[li][4 * lk], 16 * KF_AST, kpad >> 4, acc);
     __syncthreads();
@@ -588,6 +603,198 @@ __global__ __launch_bounds__(256) void kan_dx_fused_kernel(const float* __restri
   }
 }
 
+// ---- hidden layer backward in one pass (out <= 64) --------------------------------------------
+// dW and dX of a layer share the bases of every (row, input) pair and the G rows; evaluating them
+// once per pass halves the recursion (with its derivative) and the G reads of kan_dw_fused +
+// kan_dx_fused.  1-D grid of nchunk x zpad blocks (XCD-grouped as kan_dw_fused), 512 threads:
+// a block takes one 16-input chunk and walks the 64-row tiles of its row split:
+//   X, G tile -> LDS (the next tile's loads are issued before this tile's products)
+//   bases + derivatives -> As[kk][r] (derivatives stay in the registers of the pair's thread)
+//   dW chunk += G^T A                    (acc_w; waves: 4 out groups x 2 column halves)
+//   dA = G W_chunk (W chunk resident)    (acc_x; waves: 4 row groups x 2 column halves)
+//   dA -> LDS over As; Gin = SiLU' dA_base + sum_c B'_c dA_c, out through the X tile.
+constexpr int KB_THREADS = 512;
+
+__global__ __launch_bounds__(KB_THREADS) void kan_bwd_fused_kernel(const float* __restrict__ X,
+                                                                  const float* __restrict__ grid,
+                                                                  const float* __restrict__ G,
+                                                                  const float* __restrict__ WT, int64_t N, int in,
+                                                                  int out, int64_t rows_per_split, int nchunk,
+                                                                  int splits, float* __restrict__ slab,
+                                                                  float* __restrict__ Gin) {
+  __shared__ __attribute__((aligned(16))) float AD[KF_KC * KF_CST];  // As[kk][r], then dAs[r][kk]
+  __shared__ __attribute__((aligned(16))) float GG[KF_O * KF_CST];   // Gt[o][r], then Gs[r][o]
+  __shared__ __attribute__((aligned(16))) float Wt[KF_KC * KF_CST];  // W chunk [kk][o]
+  __shared__ float Xs[KF_R][KF_IC + 1];
+  __shared__ float gk[KF_IC][KF_GST];
+  const int L = blockIdx.x, q8 = L >> 3;
+  const int cid = q8 % nchunk, z = (q8 / nchunk) * 8 + (L & 7);
+  if (z >= splits) return;  // whole block, before any barrier
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lk = lane >> 4;
+  const int wr = wv & 3, wh = wv >> 2;  // 16-row (or 16-out) group, column half
+  const int i0 = cid * KF_IC;
+  const int ic = in - i0 < KF_IC ? in - i0 : KF_IC, kc = 9 * ic, kpad = (kc + 15) & ~15, nkt = kpad >> 4;
+  const int j0 = 5 * wh, nj = nkt - j0 < 0 ? 0 : (nkt - j0 > 5 ? 5 : nkt - j0);
+  const int opad = (out + 15) & ~15;
+  const int64_t K = (int64_t)KAN_K1 * in;
+  const bool vec = ic == KF_IC && (in & 3) == 0 && out == KF_O;
+  kf_fill_knots(gk, grid, i0, ic);
+  // the chunk's W^T [kk][o] stays in LDS for the whole split
+  for (int e = tid; e < kpad * KF_O; e += KB_THREADS) {
+    const int kk = e / KF_O, o = e % KF_O;
+    Wt[kk * KF_CST + o] = (kk < kc && o < out) ? WT[(int64_t)kf_col(kk, ic, i0, in) * out + o] : 0.f;
+  }
+  const int64_t rb = (int64_t)z * rows_per_split;
+  const int64_t re = rb + rows_per_split < N ? rb + rows_per_split : N;
+  f32x4 accw[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) accw[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // tile loads (vec path): X one float4 for threads < 256, G two float4 per thread
+  const int xr = tid >> 2, xi = (tid & 3) * 4;
+  auto load_x = [&](int64_t r0) {
+    float4 v = float4{0.f, 0.f, 0.f, 0.f};
+    if (tid < 256 && r0 + xr < re) v = ldg4(X + (r0 + xr) * in + i0 + xi);
+    return v;
+  };
+  auto load_g = [&](int64_t r0, int q) {  // piece q: rows (tid + 512 q) & 63, outs 4 * ((tid + 512 q) >> 6)
+    const int idx = tid + KB_THREADS * q, r = idx & 63, o4 = idx >> 6;
+    float4 v = float4{0.f, 0.f, 0.f, 0.f};
+    if (r0 + r < re) v = ldg4(G + (r0 + r) * out + 4 * o4);
+    return v;
+  };
+  float4 xv = float4{0.f, 0.f, 0.f, 0.f}, gv0 = xv, gv1 = xv;
+  if (vec && rb < re) {
+    xv = load_x(rb);
+    gv0 = load_g(rb, 0);
+    gv1 = load_g(rb, 1);
+  }
+  for (int64_t r0 = rb; r0 < re; r0 += KF_R) {
+    // ---- X and G^T tiles into LDS
+    if (vec) {
+      if (tid < 256) {
+        Xs[xr][xi] = xv.x;
+        Xs[xr][xi + 1] = xv.y;
+        Xs[xr][xi + 2] = xv.z;
+        Xs[xr][xi + 3] = xv.w;
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float4 v = q ? gv1 : gv0;
+        const int idx = tid + KB_THREADS * q, r = idx & 63, o4 = idx >> 6;
+        GG[(4 * o4) * KF_CST + r] = v.x;
+        GG[(4 * o4 + 1) * KF_CST + r] = v.y;
+        GG[(4 * o4 + 2) * KF_CST + r] = v.z;
+        GG[(4 * o4 + 3) * KF_CST + r] = v.w;
+      }
+    } else {
+      kf_stage_x(Xs, X, re, in, r0, i0, ic);
+      for (int e = tid; e < KF_R * KF_O; e += KB_THREADS) {
+        const int o = e / KF_R, r = e % KF_R;
+        GG[o * KF_CST + r] = (r0 + r < re && o < out) ? G[(r0 + r) * out + o] : 0.f;
+      }
+    }
+    __syncthreads();
+    // ---- bases (As) and derivatives (registers) of the pairs (r, ii) = (p & 63, p >> 6)
+    float dsl[2], dbs[2][KAN_NB];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = tid + KB_THREADS * h, r = p & 63, ii = p >> 6;
+      dsl[h] = 0.f;
+#pragma unroll
+      for (int c = 0; c < KAN_NB; ++c) dbs[h][c] = 0.f;
+      if (ii < ic) {
+        float b[KAN_NB], sl = 0.f;
+#pragma unroll
+        for (int c = 0; c < KAN_NB; ++c) b[c] = 0.f;
+        if (r0 + r < re) {
+          const float x = Xs[r][ii];
+          kan_bases_local<true, true>(x, gk[ii], b, dbs[h]);
+          sl = silu(x);
+          dsl[h] = silu_grad(x);
+        }
+        AD[ii * KF_CST + r] = sl;
+#pragma unroll
+        for (int c = 0; c < KAN_NB; ++c) AD[(ic + 8 * ii + c) * KF_CST + r] = b[c];
+      }
+    }
+    for (int e = tid; e < (kpad - kc) * KF_R; e += KB_THREADS) AD[(kc + e / KF_R) * KF_CST + e % KF_R] = 0.f;
+    __syncthreads();
+    // ---- the next tile's loads go out under this tile's products
+    float4 nxv = xv, ngv0 = gv0, ngv1 = gv1;
+    if (vec && r0 + KF_R < re) {
+      nxv = load_x(r0 + KF_R);
+      ngv0 = load_g(r0 + KF_R, 0);
+      ngv1 = load_g(r0 + KF_R, 1);
+    }
+    // ---- dW chunk += G^T A over the tile's rows
+    if ((KAN_ABL & 2) == 0)
+      kf_mfma_groups_n(nj, &GG[(16 * wr + li) * KF_CST + 4 * lk], &AD[(16 * j0 + li) * KF_CST + 4 * lk], 16 * KF_CST,
+                       KF_R / 16, accw);
+    __syncthreads();
+    // ---- G rows [r][o] over G^T, then dA = G W_chunk
+    if (vec) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int idx = tid + KB_THREADS * q, r = idx & 63, o4 = idx >> 6;
+        *reinterpret_cast<float4*>(&GG[r * KF_CST + 4 * o4]) = q ? gv1 : gv0;
+      }
+    } else {
+      for (int e = tid; e < KF_R * KF_O; e += KB_THREADS) {
+        const int r = e / KF_O, o = e % KF_O;
+        GG[r * KF_CST + o] = (r0 + r < re && o < out) ? G[(r0 + r) * out + o] : 0.f;
+      }
+    }
+    __syncthreads();
+    f32x4 accx[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) accx[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if ((KAN_ABL & 2) == 0)
+      kf_mfma_groups_n(nj, &GG[(16 * wr + li) * KF_CST + 4 * lk], &Wt[(16 * j0 + li) * KF_CST + 4 * lk], 16 * KF_CST,
+                       opad >> 4, accx);
+    // dA tile over As (last read by the dW products, before the barrier above); columns past kc
+    // hold products of zero-padded W rows and are never read
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      if (j < nj)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) AD[(16 * wr + 4 * lk + q) * KF_DST + 16 * (j0 + j) + li] = accx[j][q];
+    __syncthreads();
+    // ---- Gin through the X tile
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = tid + KB_THREADS * h, r = p & 63, ii = p >> 6;
+      if (ii < ic && r0 + r < re) {
+        const float* dA = AD + r * KF_DST;
+        float v = dsl[h] * dA[ii];
+#pragma unroll
+        for (int c = 0; c < KAN_NB; ++c) v += dbs[h][c] * dA[ic + 8 * ii + c];
+        Xs[r][ii] = v;
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < KF_R * ic; e += KB_THREADS) {
+      const int r = e / ic, ii = e - r * ic;
+      if (r0 + r < re) Gin[(r0 + r) * in + i0 + ii] = Xs[r][ii];
+    }
+    xv = nxv;
+    gv0 = ngv0;
+    gv1 = ngv1;
+    __syncthreads();  // Xs / GG / AD are refilled by the next tile
+  }
+  float* out_slab = slab + (int64_t)z * out * K;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int kk = 16 * (j0 + j) + li;
+    if (j >= nj || kk >= kc) continue;
+    const int64_t col = kf_col(kk, ic, i0, in);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int o = 16 * wr + 4 * lk + q;
+      if (o < out) out_slab[(int64_t)o * K + col] = accw[j][q];
+    }
+  }
+}
+
 // W[o][i] = base_w[o][i];  W[o][in + 8 i + c] = spline_w[o][i][c] * scaler[o][i]  (kan.py:145-151)
 __global__ void kan_combine_kernel(const float* __restrict__ base_w, const float* __restrict__ spline_w,
                                    const float* __restrict__ scaler, int out, int in, float* __restrict__ W,
@@ -796,6 +1003,24 @@ hipError_t kan_dx_fused(const float* X, const float* grid, const float* Gout, co
   hipLaunchKernelGGL(kan_dx_fused_kernel, dim3((unsigned)((N + KF_R - 1) / KF_R)), dim3(256), 0, s, X, grid, Gout, WT,
                      N, in, out, Gin);
   return hipGetLastError();
+}
+
+// dW (split-K slabs + fixed-order sum) and Gin of a layer with out <= 64 in one pass
+hipError_t kan_bwd_fused(const float* X, const float* grid, const float* G, const float* WT, int64_t N, int in, int out,
+                         int64_t max_splits, float* slab, float* dW, float* Gin, hipStream_t s) {
+  if (N <= 0 || in <= 0 || out <= 0 || out > KF_O || max_splits < 1) return hipErrorInvalidValue;
+  const int nchunk = (in + KF_IC - 1) / KF_IC;
+  int64_t splits = kKanBwdResidentBlocks / nchunk;  // one block per CU (LDS), one round
+  if (splits < 1) splits = 1;
+  if (splits > max_splits) splits = max_splits;
+  int64_t rps = (N + splits - 1) / splits;
+  rps = (rps + KF_R - 1) / KF_R * KF_R;
+  const int z = (int)((N + rps - 1) / rps);
+  const int64_t blocks = (int64_t)nchunk * ((z + 7) / 8 * 8);
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kan_bwd_fused_kernel, dim3((unsigned)blocks), dim3(KB_THREADS), 0, s, X, grid, G, WT, N, in, out,
+                     rps, nchunk, z, slab, Gin);
+  return slab_reduce(slab, z, (int64_t)out * KAN_K1 * in, dW, s);
 }
 
 hipError_t kan_combine(const float* base_w, const float* spline_w, const float* scaler, int out, int in, float* W,

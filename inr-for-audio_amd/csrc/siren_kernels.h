@@ -133,6 +133,9 @@ hipError_t kan_dw_fused(const float* X, const float* grid, const float* G, int64
                         int64_t max_splits, float* slab, float* dW, hipStream_t s);
 hipError_t kan_dx_fused(const float* X, const float* grid, const float* Gout, const float* WT, int64_t N, int in,
                         int out, float* Gin, hipStream_t s);
+// dW and Gin of a layer with out <= 64 in one pass (bases and G rows read once)
+hipError_t kan_bwd_fused(const float* X, const float* grid, const float* G, const float* WT, int64_t N, int in, int out,
+                         int64_t max_splits, float* slab, float* dW, float* Gin, hipStream_t s);
 // the last layer (out = 1, in <= 64): wave-per-row forward; backward with the weight-gradient
 // partials of at most `slots` row runs (slab rows of 9 in floats) and Gin, dA never formed
 hipError_t kan_head_fwd(const float* X, const float* grid, const float* W, int64_t N, int in, float* Y, hipStream_t s);
