@@ -65,6 +65,39 @@ def test_kan_inference_vs_oracle(dev):
     assert np.max(np.abs(out - ref)) < 1e-5 * max(1.0, np.max(np.abs(ref)))
 
 
+@pytest.mark.parametrize("width", [1, 3])
+def test_kan_forward_bases_bit_exact(dev, width):
+    """The forward kernels' B-spline bases are bit-identical to the torch recursion of kan.py:94-104
+    (inr_for_audio_amd.kan.bspline_bases, pinned to the reference by tests/test_kan_host.py):
+    KAN([width, 1]) with base_weight 0, spline_scaler 1 and a one-hot spline_weight outputs exactly
+    B_c(x_i) -- every other term the head kernel adds is an exact zero.  Inputs: uniform draws over
+    the grid and past it, every knot, and the floats one ulp either side of each knot."""
+    from inr_for_audio_amd.kan import KAN, bspline_bases
+    torch.manual_seed(0)
+    m = KAN([width, 1])
+    lay = m.layers[0]
+    grid = lay.grid.detach().clone()
+    kn = grid[0].numpy()
+    rng = np.random.default_rng(1)
+    x1 = np.concatenate([rng.uniform(-2.6, 2.6, 30000), kn, np.nextafter(kn, np.float32(10)),
+                         np.nextafter(kn, np.float32(-10)), [0.0, -0.0, 1e-30, -1e-30]]).astype(np.float32)
+    x = np.stack([np.roll(x1, 7 * i) for i in range(width)], 1)
+    ref = bspline_bases(torch.from_numpy(x), grid, 3).numpy()      # (n, width, 8)
+    m = m.to(dev)
+    with torch.no_grad():
+        lay.base_weight.zero_()
+        lay.spline_scaler.fill_(1.0)
+    xd = torch.from_numpy(x).to(dev).reshape(1, -1, width)
+    for i in range(width):
+        for c in range(8):
+            with torch.no_grad():
+                lay.spline_weight.zero_()
+                lay.spline_weight[0, i, c] = 1.0
+                out = m(xd).cpu().numpy().reshape(-1)
+            bad = np.flatnonzero(out != ref[:, i, c])
+            assert bad.size == 0, (i, c, bad[:5], x[bad[:5], i], out[bad[:5]], ref[bad[:5], i, c])
+
+
 def test_kan_fit_tracks_reference(dev):
     """30 full-batch steps of KAN([1, 64, 64, 1]) on gt_bach 1 s vs the reference's own loop
     (tests/golden/trajectory_kan_64.json): fp32 on both sides, losses within 1e-3 relative."""
