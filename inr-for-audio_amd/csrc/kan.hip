@@ -44,11 +44,23 @@ constexpr int KAN_K1 = 1 + KAN_NB;  // columns of A per input feature
 // so the recursion indexes registers statically: no per-lane knot gathers.  Terms whose knot
 // index falls outside the array are computed on stale window entries and discarded by a select
 // (the full recursion has no such term).
+// Forward (RCP false): every quotient a / D is the correctly rounded one, without a division:
+// with y = RN(1/D) from the per-input table inv[(k-1)*11 + j] = 1 / (g[j+k] - g[j]) (IEEE
+// divisions, once per input: kf_fill_inv), q = RN(a y), r = a - D q (exact by fma) and
+// q' = RN(q + r y) equals RN(a / D) (Markstein's theorem: y within half an ulp of 1/D, q within
+// one ulp of a/D; no underflow or overflow on these knot grids), so the bases stay bit-identical
+// to torch's (tests/test_gpu_kan.py::test_kan_forward_bases_bit_exact).
 // RCP (backward kernels): the knot-difference divisions become products with v_rcp_f32
-// reciprocals (within an ulp of the divisions; only the weight / input gradients see them -- the
-// forward keeps the exact divisions, so its bases stay bit-identical to torch's).
+// reciprocals (within an ulp of the divisions; only the weight / input gradients see them).
+__device__ __forceinline__ float kan_div(float a, float d, float y) {
+  const float q = a * y;
+  const float r = fmaf(-q, d, a);
+  return fmaf(r, y, q);
+}
+
 template <bool DERIV, bool RCP = false>
-__device__ __forceinline__ void kan_bases_local(float x, const float* __restrict__ g, float* b, float* db) {
+__device__ __forceinline__ void kan_bases_local(float x, const float* __restrict__ g, float* b, float* db,
+                                                const float* __restrict__ inv = nullptr) {
   float kn[KAN_NG];
 #pragma unroll
   for (int j = 0; j < KAN_NG; ++j) kn[j] = g[j];
@@ -88,10 +100,11 @@ __device__ __forceinline__ void kan_bases_local(float x, const float* __restrict
         l = (x - gj) * il;
         r = (gjk1 - x) * ir;
       } else {
-        il = 1.0f / (gjk - gj);
-        ir = 1.0f / (gjk1 - gj1);
-        l = (x - gj) / (gjk - gj);
-        r = (gjk1 - x) / (gjk1 - gj1);
+        const int jt = j < 0 ? 0 : (j > KAN_NG - 2 - k ? KAN_NG - 2 - k : j);  // in-table for discarded terms
+        il = inv[(k - 1) * 11 + jt];
+        ir = inv[(k - 1) * 11 + jt + 1];
+        l = kan_div(x - gj, gjk - gj, il);
+        r = kan_div(gjk1 - x, gjk1 - gj1, ir);
       }
       if constexpr (DERIV) {
         const float nd = il * w[q] + l * d[q] - ir * w[q + 1] + r * d[q + 1];
@@ -171,6 +184,17 @@ __device__ __forceinline__ void kf_fill_knots(float (*gk)[KF_GST], const float* 
   for (int e = threadIdx.x; e < ic * KAN_NG; e += blockDim.x) gk[e / KAN_NG][e % KAN_NG] = grid[i0 * KAN_NG + e];
 }
 
+// inv[ii][(k-1)*11 + j] = RN(1 / (g[j+k] - g[j])) for the knots of inputs i0 .. i0+ic-1 (IEEE
+// divisions; the forward's exact quotients, kan_div)
+constexpr int KF_VST = 33;
+__device__ __forceinline__ void kf_fill_inv(float (*inv)[KF_VST], const float* __restrict__ grid, int i0, int ic) {
+  for (int e = threadIdx.x; e < ic * 33; e += blockDim.x) {
+    const int ii = e / 33, q = e - ii * 33, k = q / 11 + 1, j = q - (k - 1) * 11;
+    const float* g = grid + (i0 + ii) * KAN_NG;
+    inv[ii][q] = (j + k < KAN_NG) ? 1.0f / (g[j + k] - g[j]) : 0.0f;
+  }
+}
+
 // As[kk][r] (pad 4) = A columns of the chunk for rows r0 + r (zero past re, and rows kc .. kpad-1
 // zero).  A wave takes one input ii and 64 consecutive rows: its knots / reciprocals are uniform
 // and the LDS writes are conflict-free.
@@ -183,6 +207,7 @@ __device__ __forceinline__ void kf_fill_a(float (*As)[KF_R + 4], const float (*X
     float b[KAN_NB], unused[KAN_NB], sl = 0.f;
     if (r0 + r < re) {
       const float x = Xs[r][ii];
+      static_assert(RCP, "the exact forward bases need the reciprocal table (kf_put_pair)");
       kan_bases_local<false, RCP>(x, gk[ii], b, unused);
       sl = silu(x);
     } else {
@@ -249,33 +274,26 @@ __device__ __forceinline__ void kf_mfma_groups_n(int nj, const float* ap, const 
   }
 }
 
-// As[r][kk] = A columns of the chunk for rows r0 + r (zero past re; columns kc .. kpad-1 zero).
-// A wave takes one input ii and 64 consecutive rows; the 8 bases go out as two b128 stores.
-__device__ __forceinline__ void kf_fill_a_rows(float (*As)[KF_AST], const float (*Xs)[KF_IC + 1],
-                                               const float (*gk)[KF_GST], int64_t re, int64_t r0, int ic, int kpad) {
-  for (int p = threadIdx.x; p < KF_R * ic; p += blockDim.x) {
-    const int r = p & (KF_R - 1), ii = p >> 6;
-    float b[KAN_NB], unused[KAN_NB], sl = 0.f;
-    if (r0 + r < re) {
-      const float x = Xs[r][ii];
-      kan_bases_local<false>(x, gk[ii], b, unused);
-      sl = silu(x);
-    } else {
+// As[r][ii] = SiLU(x), As[r][ic + 8 ii + c] = B_c(x) for the pair (r, ii) (zeros for rows past N)
+__device__ __forceinline__ void kf_put_pair(float (*As)[KF_AST], int r, int ii, int ic, float x, bool valid,
+                                            const float (*gk)[KF_GST], const float (*inv)[KF_VST]) {
+  float b[KAN_NB], unused[KAN_NB], sl = 0.f;
+  if (valid) {
+    kan_bases_local<false>(x, gk[ii], b, unused, inv[ii]);
+    sl = silu(x);
+  } else {
 #pragma unroll
-      for (int c = 0; c < KAN_NB; ++c) b[c] = 0.f;
-    }
-    As[r][ii] = sl;
-    float* d = &As[r][ic + 8 * ii];
-    if ((ic & 3) == 0) {
-      *reinterpret_cast<float4*>(d) = float4{b[0], b[1], b[2], b[3]};
-      *reinterpret_cast<float4*>(d + 4) = float4{b[4], b[5], b[6], b[7]};
-    } else {
-#pragma unroll
-      for (int c = 0; c < KAN_NB; ++c) d[c] = b[c];
-    }
+    for (int c = 0; c < KAN_NB; ++c) b[c] = 0.f;
   }
-  const int kc = 9 * ic;
-  for (int e = threadIdx.x; e < (kpad - kc) * KF_R; e += blockDim.x) As[e % KF_R][kc + e / KF_R] = 0.f;
+  As[r][ii] = sl;
+  float* d = &As[r][ic + 8 * ii];
+  if ((ic & 3) == 0) {
+    *reinterpret_cast<float4*>(d) = float4{b[0], b[1], b[2], b[3]};
+    *reinterpret_cast<float4*>(d + 4) = float4{b[4], b[5], b[6], b[7]};
+  } else {
+#pragma unroll
+    for (int c = 0; c < KAN_NB; ++c) d[c] = b[c];
+  }
 }
 
 // Y[n][o] = sum_k A[n][k] W[o][k]; grid (ceil(N/64), ceil(out/64)).  Wave w: rows 16w .. 16w+15
@@ -285,8 +303,8 @@ __global__ __launch_bounds__(256) void kan_fwd_fused_kernel(const float* __restr
                                                             float* __restrict__ Y) {
   __shared__ __attribute__((aligned(16))) float As[KF_R][KF_AST];  // [row][kk]
   __shared__ __attribute__((aligned(16))) float Ws[KF_O][KF_AST];  // [o][kk]
-  __shared__ float Xs[KF_R][KF_IC + 1];
   __shared__ float gk[KF_IC][KF_GST];
+  __shared__ float inv[KF_IC][KF_VST];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lk = lane >> 4;
   const int64_t r0 = (int64_t)blockIdx.x * KF_R;
   const int o0 = blockIdx.y * KF_O;
@@ -312,25 +330,35 @@ __global__ __launch_bounds__(256) void kan_fwd_fused_kernel(const float* __restr
   for (int i0 = 0; i0 < in; i0 += KF_IC) {
     const int ic = in - i0 < KF_IC ? in - i0 : KF_IC, kc = 9 * ic, kpad = (kc + 15) & ~15;
     kf_fill_knots(gk, grid, i0, ic);
+    kf_fill_inv(inv, grid, i0, ic);
     if (vec) {
 #pragma unroll
       for (int q = 0; q < 9; ++q) {
         const int idx = tid + 256 * q, o = idx / 36, c4 = idx % 36;
         *reinterpret_cast<float4*>(&Ws[o][4 * c4]) = wv4[q];
       }
-      Xs[xr][xi] = xv4.x;
-      Xs[xr][xi + 1] = xv4.y;
-      Xs[xr][xi + 2] = xv4.z;
-      Xs[xr][xi + 3] = xv4.w;
     } else {
-      kf_stage_x(Xs, X, N, in, r0, i0, ic);
       for (int e = tid; e < KF_O * kpad; e += blockDim.x) {
         const int o = e / kpad, kk = e - o * kpad;
         Ws[o][kk] = (o0 + o < out && kk < kc) ? W[(int64_t)(o0 + o) * K + kf_col(kk, ic, i0, in)] : 0.f;
       }
+      for (int e = tid; e < (kpad - kc) * KF_R; e += blockDim.x) As[e % KF_R][kc + e / KF_R] = 0.f;
     }
     __syncthreads();
-    kf_fill_a_rows(As, Xs, gk, N, r0, ic, kpad);
+    // A tile: the vec path's thread computes the 4 pairs whose x it loaded
+    if (vec) {
+      const bool valid = r0 + xr < N;
+      kf_put_pair(As, xr, xi, ic, xv4.x, valid, gk, inv);
+      kf_put_pair(As, xr, xi + 1, ic, xv4.y, valid, gk, inv);
+      kf_put_pair(As, xr, xi + 2, ic, xv4.z, valid, gk, inv);
+      kf_put_pair(As, xr, xi + 3, ic, xv4.w, valid, gk, inv);
+    } else {
+      for (int p = tid; p < KF_R * ic; p += blockDim.x) {
+        const int r = p & (KF_R - 1), ii = p >> 6;
+        const bool valid = r0 + r < N;
+        kf_put_pair(As, r, ii, ic, valid ? X[(r0 + r) * in + i0 + ii] : 0.f, valid, gk, inv);
+      }
+    }
     __syncthreads();
     if (vec && i0 + KF_IC < in) load_chunk(i0 + KF_IC);
     if ((KAN_ABL & 2) == 0)
@@ -354,7 +382,9 @@ __global__ __launch_bounds__(256) void kan_head_fwd_kernel(const float* __restri
                                                            const float* __restrict__ W, int64_t N, int in,
                                                            float* __restrict__ Y) {
   __shared__ float gk[64][KF_GST];
+  __shared__ float inv[64][KF_VST];
   kf_fill_knots(gk, grid, 0, in);
+  kf_fill_inv(inv, grid, 0, in);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const bool on = lane < in;
@@ -370,7 +400,7 @@ __global__ __launch_bounds__(256) void kan_head_fwd_kernel(const float* __restri
     if (on) {
       const float x = X[n * in + lane];
       float b[KAN_NB], unused[KAN_NB];
-      kan_bases_local<false>(x, gk[lane], b, unused);
+      kan_bases_local<false>(x, gk[lane], b, unused, inv[lane]);
       v = silu(x) * wb;
 #pragma unroll
       for (int c = 0; c < KAN_NB; ++c) v += b[c] * ws[c];
