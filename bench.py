@@ -109,8 +109,10 @@ def kan_work_per_row(widths):
     own VALU work is not counted, so the flop fraction is a lower bound).  Per layer l (in -> out),
     following siren_kan_train_step's dispatch:
       kan_fwd  reads X_l (4 in), writes X_{l+1} (4 out);                           2*9*in*out flop
+               (not the head below, whose forward runs in its training pass)
       l = 0:                      kan_dw  reads X_0, G_1;                           2*9*in*out
-      l > 0, out = 1, in <= 64:   kan_dw  (head) reads X_l, g, writes G_l;          2 * 2*9*in
+      l > 0, out = 1, in <= 64:   kan_dw  (head: forward, MSE gradient, backward) reads X_l,
+                                  y, writes out, g, G_l;                            3 * 2*9*in
       l > 0, out <= 64:           kan_dx  (dW + dX) reads X_l, G_{l+1}, writes G_l; 2 * 2*9*in*out
       l > 0, out > 64:            kan_dw as l = 0, and kan_dx reads X_l, G_{l+1}, writes G_l
     Weights, slabs and partials are O(width^2) per launch, not per row, and left out."""
@@ -118,14 +120,15 @@ def kan_work_per_row(widths):
     fl = {"kan_fwd": 0, "kan_dw": 0, "kan_dx": 0}
     for l in range(len(widths) - 1):
         i, o = widths[l], widths[l + 1]
+        if l > 0 and o == 1 and i <= 64:
+            by["kan_dw"] += 4 * i + 4 + 8 + 4 * i
+            fl["kan_dw"] += 54 * i
+            continue
         by["kan_fwd"] += 4 * i + 4 * o
         fl["kan_fwd"] += 18 * i * o
         if l == 0:
             by["kan_dw"] += 4 * i + 4 * o
             fl["kan_dw"] += 18 * i * o
-        elif o == 1 and i <= 64:
-            by["kan_dw"] += 4 * i + 4 + 4 * i
-            fl["kan_dw"] += 36 * i
         elif o <= 64:
             by["kan_dx"] += 4 * i + 4 * o + 4 * i
             fl["kan_dx"] += 36 * i * o
@@ -142,7 +145,7 @@ def run_kan(args, world, rank, dev, dist, lib, _lib):
     from inr_for_audio_amd.engine import KanEngine
     from inr_for_audio_amd.kan import KAN
     H = args.hidden or 64
-    per_gpu = args.coords or 441_000
+    per_gpu = -(-(args.coords or 441_000) // world) if args.strong else (args.coords or 441_000)
     n_total = per_gpu * world
     coords = torch.empty(per_gpu, 1, dtype=torch.float32, device=dev)
     _lib.check(lib.siren_coords_fill(coords.data_ptr(), per_gpu, rank * per_gpu, n_total,
@@ -191,7 +194,7 @@ def run_kan(args, world, rank, dev, dist, lib, _lib):
     result = {
         "metric": METRIC, "value": n_total * args.steps / elapsed, "unit": "coord-samples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic two-tone signal on the linspace(-1, 1) time grid; random-init KAN (seed 0)",
         "config": {"workload": f"cfg5: KAN({widths}) full-batch fit step, {per_gpu} coords/GPU", "name": "cfg5",
                    "global_batch": n_total, "coords_per_gpu": per_gpu, "widths": widths,
@@ -262,7 +265,10 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS) + ["cfg5"], default="cfg2")
     ap.add_argument("--hidden", type=int, default=None, help="override the config's width")
     ap.add_argument("--layers", type=int, default=None, help="SIREN L: sine layers incl. the first")
-    ap.add_argument("--coords", type=int, default=None, help="coordinates per GPU (weak scaling)")
+    ap.add_argument("--coords", type=int, default=None, help="coordinates per GPU (weak scaling), or the global "
+                    "batch with --strong")
+    ap.add_argument("--strong", action="store_true", help="strong scaling (cfg2 / cfg5): the global batch "
+                    "(--coords, default the config's) is fixed and split over the ranks")
     ap.add_argument("--omega0", type=float, default=None)
     ap.add_argument("--micro-batch", type=int, default=None, help="rows per fused micro-batch "
                     "(default: the whole per-GPU batch)")
@@ -300,7 +306,7 @@ def main():
     omega0 = args.omega0 if args.omega0 is not None else cfg_w0
     stream = torch.cuda.current_stream(dev).cuda_stream
     if in_dim == 1:
-        per_gpu = round_up(args.coords or cfg_coords, 128)
+        per_gpu = round_up(-(-(args.coords or cfg_coords) // world) if args.strong else (args.coords or cfg_coords), 128)
         n_total = per_gpu * world
         # this rank's shard of the global linspace grid, generated on device (bit-exact linspace)
         coords = torch.empty(per_gpu, 1, dtype=torch.float32, device=dev)
@@ -381,7 +387,8 @@ def main():
     result = {
         "metric": METRIC, "value": value, "unit": "coord-samples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+        "higher_is_better": True, "scaling": "strong" if args.strong and in_dim == 1 else "weak",
+        "vs_baseline": None, "dtype": "fp16",
         "data": f"synthetic tone mix on the {grid}; random-init weights (seed 0)",
         "config": {"workload": f"{args.config}: SIREN {layers}x{H} (in = {in_dim}) full-batch fit step, "
                                f"{per_gpu} coords/GPU",

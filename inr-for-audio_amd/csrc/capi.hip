@@ -694,10 +694,11 @@ KanWs kan_layout(const siren_kan_net* n, int64_t rows, int splits, float* base) 
   return w;
 }
 
-hipError_t kan_run_forward(const siren_kan_net* n, const siren_kan_batch* b, const KanWs& w, hipStream_t s) {
+// layers 0 .. nl-1 (nl = n_layers for inference)
+hipError_t kan_run_forward(const siren_kan_net* n, const siren_kan_batch* b, const KanWs& w, hipStream_t s, int nl) {
   const int64_t R = b->rows;
   const float* x = b->coords;
-  for (int l = 0; l < n->n_layers; ++l) {
+  for (int l = 0; l < nl; ++l) {
     const int in = n->width[l], out = n->width[l + 1];
     SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_combine(n->base_w[l], n->spline_w[l], n->scaler[l], out, in, w.W[l], w.WT[l], s));
     // X[l+1][r][o] = sum_k A[r][k] W[o][k], A = [SiLU(x) | bases(x)] recomputed in LDS
@@ -728,7 +729,7 @@ int siren_kan_forward(const siren_kan_net* net, siren_kan_batch* b, void* stream
   hipStream_t s = S(stream);
   const KanWs w = kan_layout(net, b->rows, b->splits, b->ws);
   SIREN_TRY(hipMemsetAsync(w.zero, 0, sizeof(float), s));
-  SIREN_TRY(kan_run_forward(net, b, w, s));
+  SIREN_TRY(kan_run_forward(net, b, w, s, net->n_layers));
   SIREN_TRY(head_loss(w.X[net->n_layers], 1, b->rows, w.zero, b->out, 0, 0.f, b->out, b->g, w.sse_part,
                       w.gsum_part, nullptr, s));
   return SIREN_OK;
@@ -748,28 +749,39 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, si
   const KanWs w = kan_layout(net, R, b->splits, b->ws);
   if (b->zero_grads && gr->flat) SIREN_TRY(hipMemsetAsync(gr->flat, 0, gr->flat_len * sizeof(float), s));
   SIREN_TRY(hipMemsetAsync(w.zero, 0, sizeof(float), s));
-  SIREN_TRY(kan_run_forward(net, b, w, s));
-  // MSELoss (run.py:168): out, g = 2(out - y)/N_total, squared-error partials
-  SIREN_PROF(SIREN_PROF_KAN_MISC, s, head_loss(w.X[net->n_layers], 1, b->rows, w.zero, b->target, b->n_valid,
-                                               (float)(2.0 / b->n_total), b->out, b->g, w.sse_part, w.gsum_part,
-                                               w.gmax_part, s));
-  SIREN_PROF(SIREN_PROF_KAN_MISC, s, sum_to(w.sse_part, (int)((R + 255) / 256), gr->sse, 1, s));
-  // backward (autograd of run.py:185): G = dLoss/dX[l+1], [R][out]
+  const int L = net->n_layers;
+  // a last layer of width in <= 64 after a hidden layer runs its forward, the MSE gradient and its
+  // backward in one pass (kan_head_train); otherwise forward, head_loss, backward
+  const bool head_train = L > 1 && net->width[L - 1] <= 64;
+  const float gfac = (float)(2.0 / b->n_total);
   const float* G = b->g;
-  int cur = 0;
-  for (int l = net->n_layers - 1; l >= 0; --l) {
+  int cur = 0, l_top = L - 1;
+  if (head_train) {
+    const int in = net->width[L - 1];
+    SIREN_TRY(kan_run_forward(net, b, w, s, L - 1));
+    SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_combine(net->base_w[L - 1], net->spline_w[L - 1], net->scaler[L - 1], 1, in,
+                                                   w.W[L - 1], w.WT[L - 1], s));
+    int nparts = 0;
+    SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_head_train(w.X[L - 1], net->grid[L - 1], w.W[L - 1], b->target, R, in,
+                                                    b->n_valid, gfac, w.slab_floats / (KAN_K1 * in), (R + 255) / 256,
+                                                    b->out, b->g, w.sse_part, w.slab, w.dW, w.G[cur], &nparts, s));
+    SIREN_PROF(SIREN_PROF_KAN_MISC, s, sum_to(w.sse_part, nparts, gr->sse, 1, s));
+    SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[L - 1], net->scaler[L - 1], 1, in, 1,
+                                                       gr->base_w[L - 1], gr->spline_w[L - 1], gr->scaler[L - 1], s));
+    G = w.G[cur];
+    cur ^= 1;
+    l_top = L - 2;
+  } else {
+    SIREN_TRY(kan_run_forward(net, b, w, s, L));
+    // MSELoss (run.py:168): out, g = 2(out - y)/N_total, squared-error partials
+    SIREN_PROF(SIREN_PROF_KAN_MISC, s, head_loss(w.X[L], 1, b->rows, w.zero, b->target, b->n_valid, gfac, b->out, b->g,
+                                                 w.sse_part, w.gsum_part, w.gmax_part, s));
+    SIREN_PROF(SIREN_PROF_KAN_MISC, s, sum_to(w.sse_part, (int)((R + 255) / 256), gr->sse, 1, s));
+  }
+  // backward (autograd of run.py:185): G = dLoss/dX[l+1], [R][out]
+  for (int l = l_top; l >= 0; --l) {
     const int in = net->width[l], out = net->width[l + 1];
     const float* xl = l == 0 ? b->coords : w.X[l];
-    if (out == 1 && in <= 64 && l > 0) {
-      // last layer: weight gradient and dX in one pass over the rows (rank-1 dA)
-      SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_head_bwd(xl, net->grid[l], w.W[l], G, R, in, w.slab_floats / (KAN_K1 * in), w.slab,
-                                                    w.dW, w.G[cur], s));
-      SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
-                                                         gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
-      G = w.G[cur];
-      cur ^= 1;
-      continue;
-    }
     const int64_t max_splits = w.slab_floats / ((int64_t)out * KAN_K1 * in);
     if (l > 0 && out <= 64) {
       // dW and dX = SiLU' dA_base + sum_c B'_c dA_c in one pass (bases and G read once)

@@ -9,6 +9,8 @@
 //   kan_fwd_fused  Out tile [64 rows][64 outs] = sum over input chunks of A_chunk W_chunk^T
 //   kan_dw_fused   dW chunk [out][144] += G[rows]^T A_chunk[rows]   (split-K over rows, slabs)
 //   kan_dx_fused   dA_chunk = G W_chunk (in LDS), contracted at once with the bases' derivatives
+//   kan_bwd_fused  both backward products of a chunk in one pass (out <= 64)
+//   kan_head_train the last layer (out = 1): forward, MSE gradient and backward in one pass
 // Everything is fp32 like the reference.  The bases follow kan.py:94-104's Cox-de Boor
 // recursion op for op (sub, div, mul, add; fp-contract off) on the layer's own `grid` buffer,
 // so they are bit-identical to torch's CPU result; the derivative differentiates the same
@@ -410,17 +412,26 @@ __global__ __launch_bounds__(256) void kan_head_fwd_kernel(const float* __restri
   }
 }
 
-// Backward of the last layer for dLoss/dout = g: Gin[n][i] = g_n (SiLU'(x) W[i] + sum_c B'_c(x)
-// W[in + 8 i + c]) -- dA = g W is a rank-1 product, so it is never formed -- and the weight
-// gradient's partial sums over the block's contiguous rows (its 4 waves take every 4th row, then
-// add up in a fixed order) in slab row blockIdx.x, summed later in fixed order.  Lanes own inputs.
-__global__ __launch_bounds__(256) void kan_head_bwd_kernel(const float* __restrict__ X, const float* __restrict__ grid,
-                                                           const float* __restrict__ W, const float* __restrict__ g,
-                                                           int64_t N, int in, int64_t rows_per_block,
-                                                           float* __restrict__ slab, float* __restrict__ Gin) {
+// Training step of the last layer (out = 1, in <= 64) in one pass over its rows.  Per row: the
+// forward out = SiLU(x) W[i] + sum_c B_c(x) W[in + 8 i + c] with kan_head_fwd's exact bases and
+// butterfly (so out is bit-identical to inference), the MSE gradient g = 2 (out - y) / N and the
+// squared error (run.py:160-168; rows >= n_valid contribute nothing), then the backward: Gin[n][i]
+// = g_n (SiLU'(x) W[i] + sum_c B'_c(x) W[in + 8 i + c]) (dA = g W is a rank-1 product, never
+// formed) and the weight-gradient partials -- one basis evaluation per (row, input) for the
+// forward and the backward, and no pass over X or out between them.  Blocks take >= 256 contiguous rows (one
+// slab row and one squared-error partial each); their 4 waves take every 4th row.
+__global__ __launch_bounds__(256) void kan_head_train_kernel(const float* __restrict__ X, const float* __restrict__ grid,
+                                                             const float* __restrict__ W, const float* __restrict__ y,
+                                                             int64_t N, int in, int64_t n_valid, float gfac,
+                                                             int64_t rows_per_block, float* __restrict__ out,
+                                                             float* __restrict__ g, float* __restrict__ sse_part,
+                                                             float* __restrict__ slab, float* __restrict__ Gin) {
   __shared__ float gk[64][KF_GST];
+  __shared__ float inv[64][KF_VST];
   __shared__ float part[4][KAN_K1][64];
+  __shared__ float sse_w[4];
   kf_fill_knots(gk, grid, 0, in);
+  kf_fill_inv(inv, grid, 0, in);
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t nb = (int64_t)blockIdx.x * rows_per_block;
@@ -432,33 +443,55 @@ __global__ __launch_bounds__(256) void kan_head_bwd_kernel(const float* __restri
 #pragma unroll
     for (int c = 0; c < KAN_NB; ++c) ws[c] = W[in + KAN_NB * lane + c];
   }
-  float ab = 0.f, as[KAN_NB] = {};
-  if (on)
-    for (int64_t n = nb + wv; n < ne; n += 4) {
-      const float gn = g[n];
-      const float x = X[n * in + lane];
-      float b[KAN_NB], db[KAN_NB];
-      kan_bases_local<true, true>(x, gk[lane], b, db);
-      ab += gn * silu(x);
-      float v = silu_grad(x) * wb;
+  float ab = 0.f, as[KAN_NB] = {}, sse = 0.f;
+  for (int64_t n = nb + wv; n < ne; n += 4) {
+    float x = 0.f, v = 0.f, sl = 0.f, b[KAN_NB], db[KAN_NB];
+    if (on) {
+      x = X[n * in + lane];
+      kan_bases_local<true>(x, gk[lane], b, db, inv[lane]);
+      sl = silu(x);
+      v = sl * wb;
+#pragma unroll
+      for (int c = 0; c < KAN_NB; ++c) v += b[c] * ws[c];
+    }
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const float o = (0.f + v) + 0.f;  // head_loss's accumulation of the one partial and the zero bias
+    float gn = 0.f;
+    if (n < n_valid) {
+      const float err = o - y[n];
+      sse += err * err;
+      gn = err * gfac;
+    }
+    if (lane == 0) {
+      out[n] = o;
+      g[n] = gn;
+    }
+    if (on) {
+      ab += gn * sl;
+      float d = silu_grad(x) * wb;
 #pragma unroll
       for (int c = 0; c < KAN_NB; ++c) {
         as[c] += gn * b[c];
-        v += db[c] * ws[c];
+        d += db[c] * ws[c];
       }
-      Gin[n * in + lane] = gn * v;
+      Gin[n * in + lane] = gn * d;
     }
+  }
   part[wv][0][lane] = ab;
 #pragma unroll
   for (int c = 0; c < KAN_NB; ++c) part[wv][1 + c][lane] = as[c];
+  if (lane == 0) sse_w[wv] = sse;
   __syncthreads();
-  if (wv == 0 && on) {
-    float* row = slab + (int64_t)blockIdx.x * KAN_K1 * in;
+  if (wv == 0) {
+    if (on) {
+      float* row = slab + (int64_t)blockIdx.x * KAN_K1 * in;
 #pragma unroll
-    for (int t = 0; t < KAN_K1; ++t) {
-      const float v = ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane];
-      row[t == 0 ? lane : in + KAN_NB * lane + (t - 1)] = v;
+      for (int t = 0; t < KAN_K1; ++t) {
+        const float v = ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane];
+        row[t == 0 ? lane : in + KAN_NB * lane + (t - 1)] = v;
+      }
     }
+    if (lane == 0) sse_part[blockIdx.x] = ((sse_w[0] + sse_w[1]) + sse_w[2]) + sse_w[3];
   }
 }
 
@@ -992,19 +1025,21 @@ hipError_t kan_head_fwd(const float* X, const float* grid, const float* W, int64
   return hipGetLastError();
 }
 
-// out = 1 layer backward: blocks of >= 128 contiguous rows, one slab row each (at most `slots`),
-// partial weight gradients summed in fixed order into dW
-hipError_t kan_head_bwd(const float* X, const float* grid, const float* W, const float* g, int64_t N, int in,
-                        int64_t slots, float* slab, float* dW, float* Gin, hipStream_t s) {
-  if (N <= 0 || in <= 0 || in > 64 || slots < 1) return hipErrorInvalidValue;
-  int64_t blocks = (N + 127) / 128;
+// the last layer's training pass (out = 1, in <= 64): returns the number of squared-error
+// partials written (<= max_parts, one per block) in *nparts
+hipError_t kan_head_train(const float* X, const float* grid, const float* W, const float* y, int64_t N, int in,
+                          int64_t n_valid, float gfac, int64_t slots, int64_t max_parts, float* out, float* g,
+                          float* sse_part, float* slab, float* dW, float* Gin, int* nparts, hipStream_t s) {
+  if (N <= 0 || in <= 0 || in > 64 || slots < 1 || max_parts < 1 || !nparts) return hipErrorInvalidValue;
+  int64_t blocks = (N + 255) / 256;
   if (blocks > slots) blocks = slots;
-  if (blocks > 0x7fffffff) blocks = 0x7fffffff;
+  if (blocks > max_parts) blocks = max_parts;
   const int64_t rpb = (N + blocks - 1) / blocks;
   blocks = (N + rpb - 1) / rpb;
-  hipLaunchKernelGGL(kan_head_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, grid, W, g, N, in, rpb, slab, Gin);
-  const int64_t mn = (int64_t)KAN_K1 * in;
-  return slab_reduce(slab, (int)blocks, mn, dW, s);
+  hipLaunchKernelGGL(kan_head_train_kernel, dim3((unsigned)blocks), dim3(256), 0, s, X, grid, W, y, N, in, n_valid, gfac,
+                     rpb, out, g, sse_part, slab, Gin);
+  *nparts = (int)blocks;
+  return slab_reduce(slab, (int)blocks, (int64_t)KAN_K1 * in, dW, s);
 }
 
 // dW[o][k] = sum_n G[n][o] A[n][k]: `splits` row slices into slabs, then the fixed-order slab sum

@@ -136,11 +136,13 @@ hipError_t kan_dx_fused(const float* X, const float* grid, const float* Gout, co
 // dW and Gin of a layer with out <= 64 in one pass (bases and G rows read once)
 hipError_t kan_bwd_fused(const float* X, const float* grid, const float* G, const float* WT, int64_t N, int in, int out,
                          int64_t max_splits, float* slab, float* dW, float* Gin, hipStream_t s);
-// the last layer (out = 1, in <= 64): wave-per-row forward; backward with the weight-gradient
-// partials of at most `slots` row runs (slab rows of 9 in floats) and Gin, dA never formed
+// the last layer (out = 1, in <= 64): wave-per-row forward (inference)
 hipError_t kan_head_fwd(const float* X, const float* grid, const float* W, int64_t N, int in, float* Y, hipStream_t s);
-hipError_t kan_head_bwd(const float* X, const float* grid, const float* W, const float* g, int64_t N, int in,
-                        int64_t slots, float* slab, float* dW, float* Gin, hipStream_t s);
+// the last layer's forward + MSE gradient + backward in one pass (out = 1, in <= 64); *nparts
+// squared-error partials
+hipError_t kan_head_train(const float* X, const float* grid, const float* W, const float* y, int64_t N, int in,
+                          int64_t n_valid, float gfac, int64_t slots, int64_t max_parts, float* out, float* g,
+                          float* sse_part, float* slab, float* dW, float* Gin, int* nparts, hipStream_t s);
 // W = [base_w | spline_w * scaler] as [out][9 in], and (WT != null) its transpose [9 in][out]
 hipError_t kan_combine(const float* base_w, const float* spline_w, const float* scaler, int out, int in, float* W,
                        float* WT, hipStream_t s);

@@ -53,6 +53,16 @@ def test_torchrun_two_ranks_gloo():
     assert "cpu_baseline" not in res
 
 
+def test_torchrun_two_ranks_strong_scaling():
+    """--strong: the global batch is fixed and split over the ranks (SURVEY §8e's strong curve)."""
+    res = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                "--backend", "gloo", "--steps", "2", "--warmup", "1", "--coords", "131072", "--hidden", "256",
+                "--layers", "3", "--strong", "--no-cpu-baseline"])
+    assert res["n_gpus"] == 2 and res["scaling"] == "strong" and res["value"] > 0
+    assert res["config"]["global_batch"] == 131072 and res["config"]["coords_per_gpu"] == 65536
+
+
 def test_kan_config():
     res = _run([sys.executable, "bench.py", "--config", "cfg5", "--steps", "2", "--warmup", "1", "--coords", "50000"])
     assert res["n_gpus"] == 1 and res["value"] > 0 and res["dtype"] == "fp32"
