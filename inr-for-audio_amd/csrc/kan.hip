@@ -60,19 +60,14 @@ __device__ __forceinline__ float kan_div(float a, float d, float y) {
   return fmaf(r, y, q);
 }
 
-template <bool DERIV, bool RCP = false>
-__device__ __forceinline__ void kan_bases_local(float x, const float* __restrict__ g, float* b, float* db,
-                                                const float* __restrict__ inv = nullptr) {
+// The recursion on the window: s (the span, -1 outside the grid), w[q] = B[s-3+q] and, with
+// DERIV, d[q] = B'[s-3+q] (q = 0..3).
+template <bool DERIV, bool RCP>
+__device__ __forceinline__ int kan_bases_window(float x, const float* __restrict__ g, float* w, float* d,
+                                                const float* __restrict__ inv) {
   float kn[KAN_NG];
 #pragma unroll
   for (int j = 0; j < KAN_NG; ++j) kn[j] = g[j];
-#pragma unroll
-  for (int j = 0; j < KAN_NB; ++j) b[j] = db[j] = 0.0f;
-  if constexpr ((KAN_ABL & 1) != 0) {
-#pragma unroll
-    for (int j = 0; j < KAN_NB; ++j) b[j] = db[j] = x * kn[j];
-    return;
-  }
   int s = -1;
   float kw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -80,14 +75,13 @@ __device__ __forceinline__ void kan_bases_local(float x, const float* __restrict
     const bool hit = x >= kn[j] && x < kn[j + 1];
     s = hit ? j : s;
 #pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      const int t = j - 3 + d;
-      if (t >= 0 && t < KAN_NG) kw[d] = hit ? kn[t] : kw[d];
+    for (int e = 0; e < 8; ++e) {
+      const int t = j - 3 + e;
+      if (t >= 0 && t < KAN_NG) kw[e] = hit ? kn[t] : kw[e];
     }
   }
-  if (s < 0) return;
   // window w[q] = B[s - 3 + q], q = 0..3, plus w[4] = B[s + 1] = 0
-  float w[5] = {0.0f, 0.0f, 0.0f, 1.0f, 0.0f}, d[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  float ww[5] = {0.0f, 0.0f, 0.0f, 1.0f, 0.0f}, dd[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int k = 1; k <= 3; ++k) {
 #pragma unroll
@@ -109,13 +103,34 @@ __device__ __forceinline__ void kan_bases_local(float x, const float* __restrict
         r = kan_div(gjk1 - x, gjk1 - gj1, ir);
       }
       if constexpr (DERIV) {
-        const float nd = il * w[q] + l * d[q] - ir * w[q + 1] + r * d[q + 1];
-        d[q] = ok ? nd : d[q];
+        const float nd = il * ww[q] + l * dd[q] - ir * ww[q + 1] + r * dd[q + 1];
+        dd[q] = ok ? nd : dd[q];
       }
-      const float nw = l * w[q] + r * w[q + 1];
-      w[q] = ok ? nw : w[q];
+      const float nw = l * ww[q] + r * ww[q + 1];
+      ww[q] = ok ? nw : ww[q];
     }
   }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    w[q] = ww[q];
+    if constexpr (DERIV) d[q] = dd[q];
+  }
+  return s;
+}
+
+template <bool DERIV, bool RCP = false>
+__device__ __forceinline__ void kan_bases_local(float x, const float* __restrict__ g, float* b, float* db,
+                                                const float* __restrict__ inv = nullptr) {
+#pragma unroll
+  for (int j = 0; j < KAN_NB; ++j) b[j] = db[j] = 0.0f;
+  if constexpr ((KAN_ABL & 1) != 0) {
+#pragma unroll
+    for (int j = 0; j < KAN_NB; ++j) b[j] = db[j] = x * g[j];
+    return;
+  }
+  float w[4], d[4];
+  const int s = kan_bases_window<DERIV, RCP>(x, g, w, d, inv);
+  if (s < 0) return;
 #pragma unroll
   for (int c = 0; c < KAN_NB; ++c) {
     // B[c] = w[c - s + 3] when that is a window slot

@@ -30,8 +30,9 @@ def _kan(widths, seed=0):
     return KAN(widths)
 
 
-@pytest.mark.parametrize("widths,n,mb,splits", [([1, 64, 64, 1], 2100, 1 << 20, 16), ([1, 64, 64, 1], 2100, 1000, 1),
-                                                ([1, 30, 20, 1], 3000, 1 << 20, 3), ([1, 128, 128, 1], 1024, 1 << 20, 7)])
+@pytest.mark.parametrize("widths,n,mb,splits", [
+    ([1, 64, 64, 1], 2100, 1 << 20, 16), ([1, 64, 64, 1], 2100, 1000, 1), ([1, 32, 64, 1], 44100, 1 << 20, 64),
+    ([1, 30, 20, 1], 3000, 1 << 20, 3), ([1, 128, 128, 1], 1024, 1 << 20, 7)])
 def test_kan_step_vs_oracle(dev, widths, n, mb, splits):
     from inr_for_audio_amd.engine import KanEngine
     m = _kan(widths)
