@@ -234,7 +234,9 @@ def test_train_step_act_vs_oracle(dev, H, cfg, n, a0, in_dim, mb):
     assert set(ref) == set(got)
     check_grads(f"act_step[{H}x{cfg}x{n}x{in_dim}x{mb}]", got, ref)
     out32, _ = orc.forward(p, t.numpy(), 1000.0, 30.0)
-    assert abs(eng.last_loss() - orc.mse(out32, y.numpy())) < 2e-2 * orc.mse(out32, y.numpy())
+    l32 = orc.mse(out32, y.numpy())
+    log(f"act_step_loss[{H}x{cfg}x{n}x{in_dim}x{mb}]", loss=abs(eng.last_loss() - l32) / l32)
+    assert abs(eng.last_loss() - l32) < 5e-4 * l32  # measured <= 5.8e-5
 
 
 @pytest.mark.parametrize("fl,ll", [(False, True), (True, False)])
@@ -250,11 +252,15 @@ def test_autograd_dropin_act(dev, fl, ll):
     loss.backward()
     p = orc.Params.from_state_dict(sd0, 2, 2, 0, fl, ll)
     o, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
-    assert np.max(np.abs(out.detach().cpu().numpy().reshape(-1) - o)) < 2e-2 * np.max(np.abs(o)) + 1e-3
+    oerr = np.max(np.abs(out.detach().cpu().numpy().reshape(-1) - o)) / np.max(np.abs(o))
     ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(o, y.numpy()), 1000.0, 30.0, half=True)
+    errs = {}
     for name, prm in model.named_parameters():
         assert prm.grad is not None, name
-        assert _rel(prm.grad.cpu().numpy().reshape(ref[name].shape), ref[name]) < 3e-2, name
+        errs[name] = _rel(prm.grad.cpu().numpy().reshape(ref[name].shape), ref[name])
+    log(f"autograd_dropin_act[{fl},{ll}]", out=oerr, **errs)
+    assert oerr < 2e-3, oerr                           # measured <= 3.2e-4
+    assert all(e < 2e-3 for e in errs.values()), errs  # measured <= 3.2e-4
 
 
 def _fit_snake(dev, steps, seed):
@@ -280,7 +286,9 @@ def test_fit_default_snake_first_steps_track_reference(dev):
     eng, _ = _fit_snake(dev, 20, tr["seed"])
     losses, lrs = eng.history()
     ref = np.array(tr["loss"][:20])
-    assert np.max(np.abs(losses[:8] - ref[:8]) / ref[:8]) < 5e-2
+    dev8 = np.max(np.abs(losses[:8] - ref[:8]) / ref[:8])
+    log("fit_snake_first_steps", max_rel_8=dev8)
+    assert dev8 < 2e-2  # measured 5.7e-3
     assert np.array_equal(lrs, np.array(tr["lr"][:20]))
 
 

@@ -56,7 +56,7 @@ def test_train_step_grads_vs_oracle(dev, H, L, n, w0, in_dim, mb):
     out32, _ = orc.forward(p, t.numpy(), w0, 30.0)
     l32 = orc.mse(out32, y.numpy())
     log(f"engine_loss_vs_fp32[{H}x{L}x{n}]", rel=abs(eng.last_loss() - l32) / l32)
-    assert abs(eng.last_loss() - l32) < 2e-2 * l32
+    assert abs(eng.last_loss() - l32) < 1e-4 * l32  # measured <= 2.2e-6
     # Adam applied with the device gradients is bit-exact with the oracle Adam on them
     flat = [sd0[k].astype(np.float32) for k in eng.layout.names]
     for i, k in enumerate(eng.layout.names):

@@ -87,7 +87,9 @@ def test_fit_first_steps_track_reference(dev):
     losses, lrs = eng.history()
     ref = np.array(tr["loss"][:20])
     # fp16 storage: the first steps track the fp32 reference closely
-    assert np.max(np.abs(losses[:5] - ref[:5]) / ref[:5]) < 2e-2
+    dev5 = np.max(np.abs(losses[:5] - ref[:5]) / ref[:5])
+    log("fit_3x256_first_steps", max_rel_5=dev5)
+    assert dev5 < 1e-2  # measured 2.9e-3
     assert np.array_equal(lrs, np.array(tr["lr"][:20]))
 
 
@@ -146,7 +148,9 @@ def test_fit_quality_headline_model_over_seeds(dev):
         fin_ref.append(r["snr_target"])
         drops_gpu += int(np.sum(np.diff(lrs) < 0))
         drops_ref += int(np.sum(np.diff(r["lr"]) < 0))
-        assert np.max(np.abs(losses[:3] - rl[:3]) / rl[:3]) < 2e-2, s
+        dev3 = np.max(np.abs(losses[:3] - rl[:3]) / rl[:3])
+        log(f"fit_5x1024_first_steps[{s}]", max_rel_3=dev3)
+        assert dev3 < 1e-2, s  # measured <= 2.2e-3
         first = int(np.argmax(np.diff(r["lr"]) < 0)) if np.any(np.diff(r["lr"]) < 0) else len(lrs) - 1
         assert np.array_equal(lrs[:min(first, 10)], np.array(r["lr"][:min(first, 10)])), s
     med = lambda x: float(np.median(x))  # noqa: E731

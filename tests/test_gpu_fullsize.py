@@ -70,8 +70,8 @@ def test_fullsize_microbatch_linearity(dev):
 def test_cfg2_parity_vs_torch_fp32(dev, cfg):
     """cfg2's parity size (10 s at 44.1 kHz = 441 000 coordinates, SIREN 5x1024): one fused step
     vs the same step in plain fp32 PyTorch autograd on the GPU (models.py:114-115, :241,
-    :374-394; run.py:168, :185) -- gradients within 2 % relative L2 (fp16 activation / dZ
-    storage), loss within 1e-3."""
+    :374-394; run.py:168, :185) -- gradients within 3e-3 relative L2 (fp16 activation / dZ
+    storage), loss within 1e-4."""
     from inr_for_audio_amd.engine import SirenEngine
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     n = 441000
@@ -107,5 +107,5 @@ def test_cfg2_parity_vs_torch_fp32(dev, cfg):
         r = v.grad.double()
         errs[k] = float(torch.linalg.norm(got[k].reshape(r.shape) - r) / torch.linalg.norm(r))
     log(f"cfg2_vs_torch_fp32[{cfg}]", **errs)
-    assert errs.pop("loss") <= 1e-3, errs
-    assert all(e < 2e-2 for e in errs.values()), errs
+    assert errs.pop("loss") <= 1e-4, errs  # measured 1.7e-6
+    assert all(e < 3e-3 for e in errs.values()), errs  # measured <= 6.9e-4 (fp16 storage vs fp32)

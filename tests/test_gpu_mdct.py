@@ -11,7 +11,7 @@ import torch
 from scipy.io import wavfile
 
 from oracle import siren_oracle as orc
-from errlog import check_grads
+from errlog import check_grads, log
 
 pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -58,7 +58,9 @@ def test_mdct_fit_first_steps_track_reference(dev):
         eng.step()
     losses, lrs = eng.history()
     ref = np.array(tr["loss"])
-    assert np.max(np.abs(losses[:3] - ref[:3]) / ref[:3]) < 5e-2, (losses[:5], ref[:5])
+    dev3 = np.max(np.abs(losses[:3] - ref[:3]) / ref[:3])
+    log("mdct_fit_first_steps", max_rel_3=dev3)
+    assert dev3 < 2e-2, (losses[:5], ref[:5])  # measured 3.9e-3
     assert np.array_equal(lrs, np.array(tr["lr"]))
 
 
