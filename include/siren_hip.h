@@ -325,14 +325,16 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* grads,
 /* ---- per-launch HIP-event profiling of the fused path (bench.py) --------------------
  * siren_profile_enable(n) creates 2n hipEvents; while enabled every launch made by
  * siren_train_step / siren_backward / siren_forward / siren_apply_update (and the KAN
- * entry points, kinds 8..13) is bracketed
+ * entry points, kinds 8..11) is bracketed
  * by events on its stream (eager launches only; not meant for graph capture).
  * siren_profile_read sums the elapsed time of all records of one kind (synchronises). */
 enum siren_prof_kind {
   SIREN_PROF_FIRST_FWD = 0, SIREN_PROF_INNER_FWD = 1, SIREN_PROF_HEAD = 2, SIREN_PROF_BWD_DW = 3,
   SIREN_PROF_BWD_DX = 4, SIREN_PROF_BWD_DX0 = 5, SIREN_PROF_REDUCE = 6, SIREN_PROF_UPDATE = 7,
-  /* KAN variant (siren_kan_train_step / siren_kan_forward): fused forward layer, fused
-   * weight gradient (+ slab reduce), fused dA + contraction, and the small rest */
+  /* KAN variant (siren_kan_train_step / siren_kan_forward): KAN_FWD the fused forward layers
+   * (and the inference head); KAN_DW the last layer's training pass (forward, MSE gradient,
+   * backward) and the first layer's weight gradient (+ slab reduces); KAN_DX the hidden layers'
+   * one-pass backward (dW and dX); KAN_MISC the small rest */
   SIREN_PROF_KAN_FWD = 8, SIREN_PROF_KAN_DW = 9, SIREN_PROF_KAN_DX = 10, SIREN_PROF_KAN_MISC = 11,
   SIREN_PROF_NKINDS = 12
 };
