@@ -164,11 +164,13 @@ int32_t siren_nt_tile(int32_t rows, int32_t hidden) { return nt_choose_tile(rows
 int32_t siren_dw_tile(int32_t rows, int32_t hidden) { return tn_choose_tile(rows, hidden, hidden); }
 
 int32_t siren_default_splits(int32_t rows, int32_t hidden) {
-  // aim for ~1024 blocks-worth of tiles (4 waves of resident blocks) without slices thinner
-  // than 8 K-steps
+  // 256 tiles: one round of one block per CU (GEMM + fixed-order slab reduce measured best:
+  // 2^20 x 1024 at 16 splits 1.731 ms vs 32 1.752; 220 160 x 512 at 64 splits 0.132 vs 128
+  // 0.152, tools/kernel_bench.py --dw-splits); 128 tiles: ~1024 blocks-worth.  No slice
+  // thinner than 8 K-steps.
   const int tile = tn_choose_tile(rows, hidden, hidden);
   const int ntile = (hidden / tile) * (hidden / tile);
-  int splits = (tile == 256 ? 512 : 1024) / (ntile > 0 ? ntile : 1);
+  int splits = (tile == 256 ? 256 : 1024) / (ntile > 0 ? ntile : 1);
   const int nks = rows / 64;
   const int max_splits = nks / 8 > 0 ? nks / 8 : 1;
   if (splits > max_splits) splits = max_splits;

@@ -49,7 +49,8 @@ def test_host_only_helpers(lib):
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256
     assert lib.siren_dw_tile(44288, 256) == 128 and lib.siren_nt_tile(44160, 256) == 128
-    assert lib.siren_default_splits(1 << 20, 1024) == 32        # 16 tiles x 32 slices = 512 blocks
+    assert lib.siren_default_splits(1 << 20, 1024) == 16        # 16 tiles x 16 slices = 256 blocks, one per CU
+    assert lib.siren_default_splits(220160, 512) == 64          # cfg4: 4 tiles x 64 slices
     assert lib.siren_default_splits(44160, 256) >= 1
     assert lib.siren_slab_floats(1024, 16) == 16 * 1024 * 1024
 

@@ -104,8 +104,16 @@ def main():
             sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "")
             cases[f"dw_{sfx}"] = (tile, pipe, (lambda tl=tile: run_dw(tl)), flops)
     cases["first_fwd"] = (0, 1, run_first, 0.0)
+    grad = torch.empty(H * H, device=dev)
+
+    def run_dw_reduce(splits):
+        st = run_dw(256, splits)
+        return st or lib.siren_dw_reduce(P(slabs[splits]), splits, H, 256, P(grad), 0, None, s())
+
     for sp in [int(x) for x in args.dw_splits.split(",") if x]:
         cases[f"dw_t256p0_s{sp}"] = (256, 0, (lambda sp=sp: run_dw(256, sp)), flops)
+        # the default dW K-loop (pipe 4) with its split-K reduce
+        cases[f"dwr_t256p4_s{sp}"] = (256, 4, (lambda sp=sp: run_dw_reduce(sp)), flops)
     # library calibration points (hipBLASLt through torch): the same contraction shapes with
     # no epilogue, fp16 and bf16 operands, fp16/bf16 output
     Xb, Wb, dZb = X.to(torch.bfloat16), W.to(torch.bfloat16), dZ.to(torch.bfloat16)
