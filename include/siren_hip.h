@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 6
+#define SIREN_ABI_VERSION 7
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 
@@ -367,6 +367,10 @@ enum siren_option {
 int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);
 int siren_profile_reset(void);
+/* bit k set: launches of kind k are bracketed (default all).  bench.py times its steps with only
+ * the dominant kind bracketed, so the events cost the timed region ~2 records per launch of that
+ * kind instead of ~2 per launch of the step (measured: all kinds add 2-13% to a step). */
+int siren_profile_mask(uint32_t kinds);
 int siren_profile_read(int32_t kind, double* total_ms, int64_t* count);
 
 #ifdef __cplusplus

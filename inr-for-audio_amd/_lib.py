@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_INNER = 16
 ROW_TILE = 128
 ACT_SINE, ACT_SNAKE, ACT_TANH = 0, 1, 2  # siren_act
@@ -159,6 +159,7 @@ _SIGS = {
                                             ctypes.POINTER(SirenKanBatch), _p]),
     "siren_profile_enable": (ctypes.c_int, [_i32]),
     "siren_profile_reset": (ctypes.c_int, []),
+    "siren_profile_mask": (ctypes.c_int, [ctypes.c_uint32]),
     "siren_profile_read": (ctypes.c_int, [_i32, ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(_i64)]),
 }

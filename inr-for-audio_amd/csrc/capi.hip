@@ -27,6 +27,8 @@ inline h16* B(uint16_t* p) { return (h16*)p; }
 // ---- optional per-launch HIP-event profiling (bench.py uses it inside its timed region) ----
 struct ProfState {
   bool on = false;
+  bool open = false;            // a record was begun by prof_begin
+  uint32_t mask = 0xffffffffu;  // kinds bracketed (siren_profile_mask)
   std::vector<hipEvent_t> ev;   // 2 per record
   std::vector<int> kind;
   int used = 0;
@@ -34,14 +36,17 @@ struct ProfState {
 ProfState g_prof;
 
 inline void prof_begin(int kind, hipStream_t s) {
-  if (!g_prof.on || g_prof.used >= (int)g_prof.kind.size()) return;
+  g_prof.open = false;
+  if (!g_prof.on || g_prof.used >= (int)g_prof.kind.size() || !((g_prof.mask >> kind) & 1u)) return;
   (void)hipEventRecord(g_prof.ev[2 * g_prof.used], s);
   g_prof.kind[g_prof.used] = kind;
+  g_prof.open = true;
 }
 inline void prof_end(hipStream_t s) {
-  if (!g_prof.on || g_prof.used >= (int)g_prof.kind.size()) return;
+  if (!g_prof.open) return;
   (void)hipEventRecord(g_prof.ev[2 * g_prof.used + 1], s);
   g_prof.used++;
+  g_prof.open = false;
 }
 
 #define SIREN_PROF(kind, s, expr)            \
@@ -606,6 +611,11 @@ int siren_profile_enable(int32_t max_records) {
 
 int siren_profile_reset(void) {
   g_prof.used = 0;
+  return SIREN_OK;
+}
+
+int siren_profile_mask(uint32_t kinds) {
+  g_prof.mask = kinds;
   return SIREN_OK;
 }
 
