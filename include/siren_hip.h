@@ -358,11 +358,14 @@ enum siren_prof_kind {
  *   per-store branches cost the production epilogue; DESIGN.md keeps their measurements);
  * SIREN_OPT_NT_STAGGER = persistent NT start stagger: block b idles (b % 16) * value units of
  * ~1.7k cycles before its first tile, so that the blocks' epilogue store bursts do not
- * coincide (0 = none; 0..64). */
+ * coincide (0 = none; 0..64);
+ * SIREN_OPT_NT_QUEUE = 1 (default): the ping-pong NT GEMM's persistent blocks take their tiles
+ * from a per-stream dynamic queue (8 shard heads, agent-scope atomics) in the forward modes,
+ * 2: in every mode, 0: never (the static walk b, b + G, ...).  Results are identical. */
 enum siren_option {
   SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1, SIREN_OPT_NT_PIPE = 2, SIREN_OPT_TN_PIPE = 3,
   SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_STAGGER = 5, SIREN_OPT_NT_DIAG = 6,
-  SIREN_OPT_NT_PF_DIST = 7
+  SIREN_OPT_NT_PF_DIST = 7, SIREN_OPT_NT_QUEUE = 8
 };
 int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);

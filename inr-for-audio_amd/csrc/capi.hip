@@ -590,6 +590,10 @@ int siren_set_option(int32_t option, int32_t value) {
       if (value < 0 || value > 64) return SIREN_ERR_CONFIG;
       gemm_nt_set_stagger(value);
       return SIREN_OK;
+    case SIREN_OPT_NT_QUEUE:
+      if (value < 0 || value > 2) return SIREN_ERR_CONFIG;
+      gemm_nt_set_queue(value);
+      return SIREN_OK;
   }
   return SIREN_ERR_CONFIG;
 }

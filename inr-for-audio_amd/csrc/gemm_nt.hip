@@ -108,8 +108,22 @@ struct NtLds {
   static constexpr int HW = BIAS + (nt_is_fwd(MODE) ? Cfg::VEC : 0);
   static constexpr int A = HW + (HEAD ? Cfg::VEC : 0);
   static constexpr int PF = A + (MODE == NT_FWD_SNAKE ? Cfg::VEC : 0);
-  static constexpr int SIZE = PF + (Cfg::PF ? 256 : 0);
+  static constexpr int QS = PF + (Cfg::PF ? 256 : 0);  // dynamic tile queue: 2 tile ids
+  static constexpr int SIZE = QS + 16;
 };
+
+// Tile-queue counter set: 8 shard heads and the done counter 128 B apart, then 64 scratch words
+// per shard
+constexpr int kQueueHeads = 9 * 32, kQueueSet = kQueueHeads + 8 * 64;
+
+// Dynamic tile queue (ping-pong K-loop).  A pull is one returning agent-scope atomic add on the
+// block's shard head, issued at the start of a tile's epilogue and consumed after it: hipcc's
+// own waitcnt then lets the epilogue's stores stay in flight (vmcnt retires in issue order).
+// Wave 0 issues it with every lane active (lane 0 adds 1 to the head, lanes 1..63 add 0 to
+// the shard's scratch words, so the head sees one add per pull and the returned VGPR is
+// written in every lane).  The pull's VGPR lives only across the epilogue, not across the
+// K-loop (no register to spare).  (An inline-asm pull whose VGPR hipcc does not know is in
+// flight is unsafe: a register copy at a branch join reads it before it lands.)
 
 constexpr bool nt_is_dx0(int m) { return m == NT_DX0 || m == NT_DX0_SNAKE; }
 
@@ -122,7 +136,8 @@ constexpr int epilogue_stores() {
                                                   : 0;
 }
 
-template <class Cfg, int MODE, bool HEAD>
+// QUEUE (ping-pong K-loop only): tiles from the dynamic queue p.tileq instead of the static walk
+template <class Cfg, int MODE, bool HEAD, bool QUEUE = false>
 __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, BK = Cfg::BK, WN = Cfg::WN;
   constexpr int TM = Cfg::TM, TN = Cfg::TN, SM = Cfg::SM, SN = Cfg::SN;
@@ -142,13 +157,22 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // hold consecutive tile ids, i.e. they share X row-blocks in L2 at the same time.
   const int G = gridDim.x;
   const int bp = xcd_remap(blockIdx.x, G);
-  const int my_tiles = (p.diag & 512) ? 0 : (ntiles - bp + G - 1) / G;  // diag bit 9: no tiles
+  // measurement-only ablation bits; the queue kernel is launched with none
+  const int diag = (Cfg::PP && QUEUE) ? 0 : p.diag;
+  const int my_tiles = (diag & 512) ? 0 : (ntiles - bp + G - 1) / G;  // diag bit 9: no tiles
+  // Dynamic tile queue (ping-pong K-loop, NtParams::tileq).  With the static walk the four
+  // blocks that share a row band of X drift apart over the launch and X is fetched ~1.6x from
+  // HBM.  Instead the blocks of one shard (blockIdx % 8: one XCD under round-robin
+  // dispatch -- speed only, any placement is correct) pull the tiles of their contiguous
+  // eighth of the grid in order, so the blocks holding one row band are the ones that started
+  // it at the same time.
+  constexpr bool dyn = Cfg::PP && QUEUE;
   // Start stagger: blocks that run in lockstep hit their epilogues together and their
   // stores then arrive as one chip-wide burst; spreading the starts over a tile's duration
   // spreads the bursts.
   for (int i = (bp & 15) * p.stagger; i > 0; --i) __builtin_amdgcn_s_sleep(27);
-  auto tile_of = [&](int i, int& m0, int& n0) {
-    const int g = bp + i * G;
+  // global tile id g -> origin; the static walk's i-th tile of this block is g = bp + i * G
+  auto tile_of = [&](int g, int& m0, int& n0) {
     const int tm = tn_pow2 ? (g >> tn_shift) : g / tiles_n;
     m0 = tm * BM;
     n0 = (g - tm * tiles_n) * BN;
@@ -171,10 +195,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   }
   auto stage = [&](int ti, int kt, int slot) {
     int m0, n0;
-    tile_of(ti, m0, n0);
+    tile_of(bp + ti * G, m0, n0);
     const char* xs = smem + slot * Cfg::STAGE + wave * Cfg::XINSTR * 1024;
     const char* ws = smem + slot * Cfg::STAGE + Cfg::XBYTES + wave * Cfg::WINSTR * 1024;
-    const h16* xk = p.X + (size_t)((p.diag & 1) ? (m0 & (4 * BM - 1)) : m0) * K + kt * BK;
+    const h16* xk = p.X + (size_t)((diag & 1) ? (m0 & (4 * BM - 1)) : m0) * K + kt * BK;
     const h16* wk = p.W + (size_t)n0 * K + kt * BK;
 #pragma unroll
     for (int j = 0; j < Cfg::XINSTR; ++j) glds16_asm(xk + xrel[j], lds_addr(xs + j * 1024));
@@ -188,7 +212,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       while (pk >= p.K / BK) { pk -= p.K / BK; ++pt; }
       if (pt >= my_tiles) pt = ti, pk = kt;
       int pm0, pn0;
-      tile_of(pt, pm0, pn0);
+      tile_of(bp + pt * G, pm0, pn0);
 #pragma unroll
       for (int j = 0; j < Cfg::PF; ++j) {
         const int r = (wave * Cfg::PF + j) * 32 + (lane & 31);
@@ -247,9 +271,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   constexpr int PRE_J = nt_is_fwd(MODE) ? 0 : (MODE == NT_DX ? SM : SM / 2);
   uint4 cp_in[PRE_J > 0 ? PRE_J : 1][SN / 2];
   float t_in[SM][2];
-  auto pre = [&](int ti) {
+  auto pre = [&](int g) {
     int m0, n0;
-    tile_of(ti, m0, n0);
+    tile_of(g, m0, n0);
     const int npc = n0 + wn * TN + swap16_col(lane);
     const int mrow0 = m0 + wm * TM + (lane & 15);
     if constexpr (!nt_is_fwd(MODE)) {
@@ -268,9 +292,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       }
     }
   };
-  auto epilogue = [&](int ti) {
+  auto epilogue = [&](int g) {
     int m0, n0;
-    tile_of(ti, m0, n0);
+    tile_of(g, m0, n0);
     const int tm = m0 / BM, tn = n0 / BN;
     const int npc = n0 + wn * TN + swap16_col(lane);      // swapped layout: this lane's piece
     const int mrow0 = m0 + wm * TM + (lane & 15);
@@ -468,16 +492,42 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     // operand bases of the current tile (0) and the next one (1), set once per tile:
     // no division or 64-bit product in the per-phase scalar work
     const h16 *x0 = p.X, *x1 = p.X, *w0 = p.W, *w1 = p.W;
+    // This block's current and next tile (global ids); the next one exists while g_next < g_lim.
+    // Static walk: bp, bp + G, ...  Queue: shard s = blockIdx % 8 (one XCD under round-robin
+    // dispatch -- speed only, any placement is correct) pulls tiles [s, s + 1) * ntiles / 8 in
+    // order, so the blocks holding one row band of X are the ones that started it together.
+    const int shard = blockIdx.x & 7;
+    const int q_lo = (int)((long)shard * ntiles / 8);
+    const int g_lim = dyn ? (int)((long)(shard + 1) * ntiles / 8) : (my_tiles > 0 ? ntiles : 0);
+    int* const qhead = p.tileq + shard * 32;  // dereferenced only when dyn
+    int* const qslot = (int*)(smem + Lay::QS);
+    int g_cur = bp, g_next = bp + G;
+    if (dyn) {
+      if (tid == 0) {
+        qslot[0] = q_lo + __hip_atomic_fetch_add(qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        qslot[1] = q_lo + __hip_atomic_fetch_add(qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      lds_barrier();
+      g_cur = __builtin_amdgcn_readfirstlane(qslot[0]);
+      g_next = __builtin_amdgcn_readfirstlane(qslot[1]);
+      lds_barrier();  // read by every wave before wave 0 reuses the slot
+    }
+    auto more = [&](int) { return g_next < g_lim; };
     auto set_tiles = [&](int ti) {
-      auto bases = [&](int t, const h16*& xb, const h16*& wb) {
+      if (ti > 0) {
+        g_cur = g_next;
+        // queue: the pull tile_end(ti - 1) left in the slot
+        g_next = dyn ? __builtin_amdgcn_readfirstlane(qslot[0]) : g_next + G;
+      }
+      auto bases = [&](int g, const h16*& xb, const h16*& wb) {
         int m0, n0;
-        tile_of(t, m0, n0);
-        const int xm0 = (p.diag & 1) ? (m0 & (4 * BM - 1)) : m0;
+        tile_of(g, m0, n0);
+        const int xm0 = (diag & 1) ? (m0 & (4 * BM - 1)) : m0;
         xb = p.X + (size_t)xm0 * K;
-        wb = p.W + (size_t)((p.diag & 4) ? 0 : n0) * K;  // diag bit 2: one W column tile (L2-resident W)
+        wb = p.W + (size_t)((diag & 4) ? 0 : n0) * K;  // diag bit 2: one W column tile (L2-resident W)
       };
-      bases(ti, x0, w0);
-      bases(ti + 1 < my_tiles ? ti + 1 : ti, x1, w1);
+      bases(g_cur, x0, w0);
+      bases(g_next < g_lim ? g_next : g_cur, x1, w1);
     };
     auto issue = [&](int sel, int kt, int slot, auto pcc) {
       constexpr int PC = decltype(pcc)::value;
@@ -523,20 +573,39 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                 __builtin_amdgcn_mfma_f32_16x16x32_f16(a, xf[jl][kk], acc[2 * NH + il][4 * MH + jl], 0, 0, 0);
           }
     };
-    auto tile_end = [&](int ti) {
-      pre(ti);
-      if (!(p.diag & 1024)) epilogue(ti);  // diag bit 10: no epilogue (timing only)
+    auto tile_end = [&](int) {
+      // both groups are aligned here
+      pre(g_cur);
+      int pend = 0;  // the tile after next
+      if (dyn && wave == 0)
+        pend = __hip_atomic_fetch_add(lane == 0 ? qhead : p.tileq + kQueueHeads + shard * 64 + lane, lane == 0 ? 1 : 0,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!(diag & 1024)) epilogue(g_cur);  // diag bit 10: no epilogue (timing only)
+      if constexpr (dyn) {
+        if (tid == 0) qslot[0] = q_lo + pend;
+        lds_barrier();
+      }
 #pragma unroll
       for (int i = 0; i < SN; ++i)
 #pragma unroll
         for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(my_tiles, nk, wm, issue, read, mma, set_tiles,
-                                                         tile_end);
+    pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(g_cur < g_lim, nk, wm, issue, read, mma, set_tiles,
+                                                         tile_end, more);
+    if (dyn && tid == 0) {
+      // every pull of this block has returned (the loop ends with vmcnt(0)); the last block
+      // to get here re-zeroes the queue for the next launch on this stream
+      int* const done = p.tileq + 8 * 32;
+      if (__hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+        for (int q = 0; q < 8; ++q) __hip_atomic_store(p.tileq + q * 32, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   } else {
     mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR + Cfg::PF, SN, SM,
                         epilogue_stores<Cfg, MODE>(), Cfg::PF>(
-        my_tiles, K / BK, acc, stage, frags, pre, epilogue, p.stamps);
+        my_tiles, K / BK, acc, stage, frags, [&](int ti) { pre(bp + ti * G); },
+        [&](int ti) { epilogue(bp + ti * G); }, p.stamps);
   }
 }
 
@@ -550,6 +619,36 @@ static int g_nt_pf_dist = 2;
 void gemm_nt_set_pf_dist(int d) { g_nt_pf_dist = d; }
 void gemm_nt_set_diag(int bits) { g_nt_diag = bits; }
 static unsigned long long* g_nt_stamps = nullptr;
+static int g_nt_queue = 1;  // 0 off, 1 forward modes, 2 every ping-pong mode
+void gemm_nt_set_queue(int v) { g_nt_queue = v; }
+
+// Tile-queue counters: one set per (device, stream), so launches that share a set are ordered
+// by their stream.  A set is 8 shard heads and a done counter, 128 B apart, zero between
+// launches (statically zero; each launch's last block re-zeroes it).
+constexpr int kQueueSets = 16;
+__device__ int g_ntq[kQueueSets][kQueueSet];
+static int* nt_queue(hipStream_t s) {
+  static struct { int dev; hipStream_t s; } used[kQueueSets];
+  static int nused = 0;
+  static int* base[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!base[dev]) {
+    void* b = nullptr;
+    if (hipGetSymbolAddress(&b, HIP_SYMBOL(g_ntq)) != hipSuccess) return nullptr;
+    base[dev] = (int*)b;
+  }
+  int k = 0;
+  for (; k < nused; ++k)
+    if (used[k].dev == dev && used[k].s == s) break;
+  if (k == nused) {
+    if (nused == kQueueSets) return nullptr;  // more streams than sets: static walk
+    used[nused++] = {dev, s};
+  }
+  int per_dev = 0;  // index of this stream among the device's sets
+  for (int j = 0; j < k; ++j) per_dev += used[j].dev == dev;
+  return base[dev] + per_dev * kQueueSet;
+}
 #ifdef SIREN_NT_STAMPS
 // diagnostic builds only: [grid][256 tiles][4] u64 device buffer, or null to stop recording
 extern "C" void siren_debug_nt_stamps(void* buf) { g_nt_stamps = (unsigned long long*)buf; }
@@ -574,6 +673,16 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
   }
   const int cap = g_nt_grid_cap > 0 ? g_nt_grid_cap : g_num_cus * Cfg::BPC;
   const int grid = persistent ? (ntiles < cap ? ntiles : cap) : ntiles;
+  // the queue's shards are blockIdx % 8: every shard must have blocks
+  // (measured: the forward gains 3-4%; dX is unchanged and dX0 loses 2%, its K-loop spills)
+  const bool want = g_nt_queue == 2 || (g_nt_queue == 1 && nt_is_fwd(MODE));
+  p.tileq = (Cfg::PP && want && !p.diag && grid % 8 == 0) ? nt_queue(s) : nullptr;
+  if constexpr (Cfg::PP) {
+    if (p.tileq) {
+      hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD, true>), dim3(grid), dim3(Cfg::THREADS), 0, s, p);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD>), dim3(grid), dim3(Cfg::THREADS), 0, s, p);
   return hipGetLastError();
 }

@@ -285,6 +285,8 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
 //   set_tiles(ti)                     operand bases of tiles ti and ti + 1 (ti again at the
 //                                     block's last tile)
 //   tile_end(ti)                      epilogue with both groups aligned (equal barrier count)
+//   more(ti)                          after tile_end(ti): does the block have a tile ti + 1?
+//                                     (block-uniform; a static walk or the dynamic tile queue)
 template <int PH>
 using phase_t = std::integral_constant<int, PH>;
 
@@ -295,12 +297,13 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int E, int WAITMASK, class IssueFn, class ReadFn, class MmaFn, class SetFn, class EndFn>
-__device__ __forceinline__ void pingpong_tiles(int ntiles, int nk, int grp, IssueFn&& issue,
+template <int E, int WAITMASK, class IssueFn, class ReadFn, class MmaFn, class SetFn, class EndFn,
+          class MoreFn>
+__device__ __forceinline__ void pingpong_tiles(bool any, int nk, int grp, IssueFn&& issue,
                                                 ReadFn&& read, MmaFn&& mma, SetFn&& set_tiles,
-                                                EndFn&& tile_end) {
+                                                EndFn&& tile_end, MoreFn&& more) {
   static_assert(E >= 0 && 8 + E < 64, "vmcnt immediate");
-  if (ntiles <= 0 || nk <= 0) return;
+  if (!any || nk <= 0) return;
   set_tiles(0);
   issue(0, 0, 0, phase_t<0>{});
   issue(0, 0, 0, phase_t<1>{});
@@ -340,14 +343,16 @@ __device__ __forceinline__ void pingpong_tiles(int ntiles, int nk, int grp, Issu
     phase(phase_t<2>{});
     phase(phase_t<3>{});
   };
-  for (int ti = 0; ti < ntiles; ++ti) {
+  for (int ti = 0;; ++ti) {
     if (ti == 0) kstep(0, std::false_type{});
     else kstep(0, std::true_type{});
     for (int kt = 1; kt < nk; ++kt) kstep(kt, std::false_type{});
-    if (grp == 0) pp_barrier();                     // meet group 1's last barrier: aligned
+    if (grp == 0) pp_barrier();  // meet group 1's last barrier: aligned
     tile_end(ti);
-    if (ti + 1 < ntiles) set_tiles(ti + 1);
-    if (grp == 1 && ti + 1 < ntiles) pp_barrier();  // group 1 one barrier behind again
+    const bool next = more(ti);
+    if (!next) break;
+    set_tiles(ti + 1);
+    if (grp == 1) pp_barrier();  // group 1 one barrier behind again
   }
   wait_vmcnt<0>();
 }

@@ -220,7 +220,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
           acc[4 * IH + il][j] =
               __builtin_amdgcn_mfma_f32_16x16x32_f16(af[il], bf[j], acc[4 * IH + il][j], 0, 0, 0);
     };
-    pingpong_tiles<0, 0xA>(1, nkl, wm, issue, read, mma, [](int) {}, [](int) {});
+    pingpong_tiles<0, 0xA>(true, nkl, wm, issue, read, mma, [](int) {}, [](int) {},
+                               [](int) { return false; });
     }
   } else {
     mfma_pipeline<Cfg::S, false, BK / 32, Cfg::YINSTR + Cfg::ZINSTR>(ks_end - ks_begin, acc, stage, frags);

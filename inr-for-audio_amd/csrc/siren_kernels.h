@@ -45,6 +45,9 @@ struct NtParams {
   int diag;             // SIREN_OPT_NT_DIAG ablation bits (0 in production)
   int stagger;          // persistent grid: block b idles (b % 16) * stagger * ~1.7k cycles first
   unsigned long long* stamps;  // SIREN_NT_STAMPS diagnostic builds only
+  // ping-pong K-loop only: dynamic tile queue (null = static walk b, b + G, ...).  8 shard heads
+  // and one done counter, 128 B apart, zero at launch; the last block to finish re-zeroes them
+  int* tileq;
 };
 
 int nt_choose_tile(int M, int N);
@@ -57,6 +60,7 @@ void gemm_nt_set_grid_cap(int cap);  // persistent grid size override (0 = #CUs)
 void gemm_nt_set_pf_dist(int d);   // SIREN_OPT_NT_PF_DIST
 void gemm_nt_set_diag(int bits);     // SIREN_OPT_NT_DIAG (measurement-only ablations)
 void gemm_nt_set_stagger(int units); // persistent grid start stagger (see NtParams::stagger)
+void gemm_nt_set_queue(int on);       // SIREN_OPT_NT_QUEUE: dynamic tile queue (ping-pong K-loop)
 struct TnParams {
   const h16* Y;   // [R][Hin]   layer input (A role: dW column index k)
   const h16* dZ;  // [R][Hout]  layer pre-activation gradient (B role: dW row index o)
