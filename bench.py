@@ -47,12 +47,19 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-KIND_MATCH = {  # profile kind -> substrings of the rocprofv3 kernel name
-    "inner_fwd": ("gemm_nt_kernel", ", 0, false>"),
-    "bwd_dx": ("gemm_nt_kernel", ", 1, false>"),
-    "bwd_dx0": ("gemm_nt_kernel", ", 2, false>"),
-    "bwd_dw": ("gemm_tn_kernel", ""),
+KIND_MATCH = {  # profile kind -> (kernel-name substring, accepted template-argument tails)
+    # gemm_nt_kernel<Cfg, MODE, HEAD[, QUEUE]>: the head-less forward, statically walked or
+    # from the dynamic tile queue (gemm_nt.hip)
+    "inner_fwd": ("gemm_nt_kernel", (", 0, false>", ", 0, false, true>")),
+    "bwd_dx": ("gemm_nt_kernel", (", 1, false>", ", 1, false, true>")),
+    "bwd_dx0": ("gemm_nt_kernel", (", 2, false>", ", 2, false, true>")),
+    "bwd_dw": ("gemm_tn_kernel", ("",)),
 }
+
+
+def kind_match(kind: str, kernel_name: str) -> bool:
+    a, tails = KIND_MATCH[kind]
+    return a in kernel_name and any(t in kernel_name for t in tails)
 
 
 def pmc_traffic(kind: str):
@@ -66,10 +73,8 @@ def pmc_traffic(kind: str):
         return None, None
     with open(files[-1]) as f:
         pmc = json.load(f)
-    a, b = KIND_MATCH[kind]
-
     def avg(counter):
-        vals = [v["avg_KB_per_dispatch"] for k, v in pmc.get(counter, {}).items() if a in k and b in k]
+        vals = [v["avg_KB_per_dispatch"] for k, v in pmc.get(counter, {}).items() if kind_match(kind, k)]
         return sum(vals) / len(vals) if vals else None
     fetch, write = avg("FETCH_SIZE"), avg("WRITE_SIZE")
     if fetch is None or write is None:
@@ -87,8 +92,7 @@ def pmc_mfma_util(kind: str):
         return None
     with open(files[-1]) as f:
         pmc = json.load(f)
-    a, b = KIND_MATCH[kind]
-    vals = [v["mfma_util"] for k, v in pmc.items() if a in k and b in k]
+    vals = [v["mfma_util"] for k, v in pmc.items() if kind_match(kind, k)]
     return sum(vals) / len(vals) if vals else None
 
 
