@@ -573,8 +573,22 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                 __builtin_amdgcn_mfma_f32_16x16x32_f16(a, xf[jl][kk], acc[2 * NH + il][4 * MH + jl], 0, 0, 0);
           }
     };
-    auto tile_end = [&](int) {
+#ifdef SIREN_NT_STAMPS
+    // diagnostic builds only (tools/nt_stamps.py): per tile {start, global tile id, end of the
+    // MFMAs, end of the epilogue} on the chip-wide 100 MHz real-time counter
+    unsigned long long st_prev = 0;
+    auto rt_now = [] {
+      unsigned long long t;
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+      return t;
+    };
+    if (p.stamps) st_prev = rt_now();
+#endif
+    auto tile_end = [&](int ti) {
       // both groups are aligned here
+#ifdef SIREN_NT_STAMPS
+      const unsigned long long st_m = p.stamps ? rt_now() : 0;
+#endif
       pre(g_cur);
       int pend = 0;  // the tile after next
       if (dyn && wave == 0)
@@ -585,6 +599,19 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         if (tid == 0) qslot[0] = q_lo + pend;
         lds_barrier();
       }
+#ifdef SIREN_NT_STAMPS
+      if (p.stamps) {
+        const unsigned long long st_e = rt_now();
+        if (tid == 0 && ti < 256) {
+          unsigned long long* sp = p.stamps + ((size_t)blockIdx.x * 256 + ti) * 4;
+          sp[0] = st_prev;
+          sp[1] = (unsigned long long)g_cur;
+          sp[2] = st_m;
+          sp[3] = st_e;
+        }
+        st_prev = st_e;
+      }
+#endif
 #pragma unroll
       for (int i = 0; i < SN; ++i)
 #pragma unroll

@@ -35,6 +35,8 @@ def main():
                     "NT cases (1: L2-resident X; pipe 4: 512 no tiles, 1024 no epilogue); timing only")
     ap.add_argument("--pf-dists", default="2", help="SIREN_OPT_NT_PF_DIST values for NT pipe 5")
     ap.add_argument("--dw-splits", default="", help="extra dW cases at these split-K counts (256 tile)")
+    ap.add_argument("--grids", default="", help="SIREN_OPT_NT_GRID persistent grid sizes to add as extra "
+                    "ping-pong NT cases (measurement: CU-count scaling)")
     ap.add_argument("--queue-ab", action="store_true", help="add a static-walk (SIREN_OPT_NT_QUEUE 0) "
                     "twin of every ping-pong NT case")
     args = ap.parse_args()
@@ -151,6 +153,14 @@ def main():
                     cases[f"{k}_q{q}"] = c
                     queue[f"{k}_q{q}"] = q
                     stagger[f"{k}_q{q}"] = stagger.get(k, 0)
+    grid = {k: 0 for k in cases}
+    for v in [int(x) for x in args.grids.split(",") if x]:
+        for k, c in list(cases.items()):
+            if k.startswith(("fwd", "dx")) and "p4" in k and diag.get(k, 0) == 0 and queue.get(k, 1) == 1 \
+                    and grid.get(k, 0) == 0 and stagger.get(k, 0) == 0:
+                cases[f"{k}_g{v}"] = c
+                grid[f"{k}_g{v}"] = v
+                stagger[f"{k}_g{v}"] = 0
     times = {k: [] for k in cases}
     for _ in range(args.rounds):
         for name, (tile, pipe, fn, _) in cases.items():
@@ -167,6 +177,7 @@ def main():
             _lib.check(lib.siren_set_option(5, stagger[name]), "stagger option")
             _lib.check(lib.siren_set_option(6, diag.get(name, 0)), "diag option")
             _lib.check(lib.siren_set_option(8, queue.get(name, 1)), "queue option")
+            _lib.check(lib.siren_set_option(4, grid.get(name, 0)), "grid option")
             if pfd.get(name, 0):
                 lib.siren_set_option(7, pfd[name])
             lib.siren_set_option(0, tile if not name.startswith("dw") else 0)
@@ -186,6 +197,7 @@ def main():
     lib.siren_set_option(5, 0)
     lib.siren_set_option(6, 0)
     lib.siren_set_option(8, 1)
+    lib.siren_set_option(4, 0)
     lib.siren_set_option(0, 0)
     lib.siren_set_option(2, -1)
     lib.siren_set_option(3, -1)
