@@ -42,6 +42,9 @@
 #ifndef SIREN_WPOL
 #define SIREN_WPOL 0  // ... of the W operand
 #endif
+#ifndef SIREN_FULLLINE
+#define SIREN_FULLLINE 0  // forward epilogue stores as whole 128-B lines (measurement builds)
+#endif
 
 namespace siren {
 
@@ -315,6 +318,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
         const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
+        uint4 yp[SN / 2], cpk[SN / 2], epk[SN / 2];
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
           uint2 ys[2], cs[2], es[2];
@@ -360,9 +364,36 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             if constexpr (HEAD)
               hp[j] += s[0] * hw[i].x + s[1] * hw[i].y + s[2] * hw[i].z + s[3] * hw[i].w;
           }
-          st16(p.Y + rowoff + npc + pp * 32, swap16_pair(ys[0], ys[1]));
-          st16(p.C + rowoff + npc + pp * 32, swap16_pair(cs[0], cs[1]));
-          if constexpr (MODE == NT_FWD_SNAKE) st16(p.E + rowoff + npc + pp * 32, swap16_pair(es[0], es[1]));
+          yp[pp] = swap16_pair(ys[0], ys[1]);
+          cpk[pp] = swap16_pair(cs[0], cs[1]);
+          if constexpr (MODE == NT_FWD_SNAKE) epk[pp] = swap16_pair(es[0], es[1]);
+        }
+        if constexpr (SIREN_FULLLINE && SN == 4) {
+          // lanes l and l^8 (rows r, r^8 of the subtile) trade one 16-B piece so that each store
+          // instruction writes 8 whole 128-B row segments instead of 16 half ones:
+          // A = rows 0..7 (low lanes their piece 0, high lanes the partner's piece 1), B = rows 8..15
+          const bool hi = (lane & 8) != 0;
+          const size_t ra = (size_t)(m0 + wm * TM + j * 16 + (lane & 7)) * N + npc + (hi ? 32 : 0);
+          auto fl_store = [&](h16* dst, const uint4 (&pc)[SN / 2]) {
+            const uint4 send = hi ? pc[0] : pc[1];
+            uint4 recv;
+            recv.x = __builtin_amdgcn_update_dpp(0, (int)send.x, 0x128, 0xf, 0xf, false);  // row_ror:8
+            recv.y = __builtin_amdgcn_update_dpp(0, (int)send.y, 0x128, 0xf, 0xf, false);
+            recv.z = __builtin_amdgcn_update_dpp(0, (int)send.z, 0x128, 0xf, 0xf, false);
+            recv.w = __builtin_amdgcn_update_dpp(0, (int)send.w, 0x128, 0xf, 0xf, false);
+            st16(dst + ra, hi ? recv : pc[0]);
+            st16(dst + ra + (size_t)8 * N, hi ? pc[1] : recv);
+          };
+          fl_store(p.Y, yp);
+          fl_store(p.C, cpk);
+          if constexpr (MODE == NT_FWD_SNAKE) fl_store(p.E, epk);
+        } else {
+#pragma unroll
+          for (int pp = 0; pp < SN / 2; ++pp) {
+            st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
+            st16(p.C + rowoff + npc + pp * 32, cpk[pp]);
+            if constexpr (MODE == NT_FWD_SNAKE) st16(p.E + rowoff + npc + pp * 32, epk[pp]);
+          }
         }
       }
       if constexpr (HEAD) {

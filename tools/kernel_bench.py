@@ -39,11 +39,13 @@ def main():
                     "ping-pong NT cases (measurement: CU-count scaling)")
     ap.add_argument("--queue-ab", action="store_true", help="add a static-walk (SIREN_OPT_NT_QUEUE 0) "
                     "twin of every ping-pong NT case")
+    ap.add_argument("--lib", default="", help="load this library instead of the product one "
+                    "(a measurement build from __graft_entry__.build_diagnostic)")
     args = ap.parse_args()
     import __graft_entry__ as ge
     ge.build()
     from inr_for_audio_amd import _lib
-    lib = _lib.load()
+    lib = _lib.load(os.path.join(ROOT, args.lib)) if args.lib else _lib.load()
     dev = torch.device("cuda:0")
     R, H = args.rows, args.hidden
     s = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
