@@ -274,6 +274,25 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   constexpr int PRE_J = nt_is_fwd(MODE) ? 0 : (MODE == NT_DX ? SM : SM / 2);
   uint4 cp_in[PRE_J > 0 ? PRE_J : 1][SN / 2];
   float t_in[SM][2];
+  // SIREN_FULLLINE (measurement builds): Cprev of row subtile j as two whole-line loads, rows
+  // 0..7 (A) and 8..15 (B) of the subtile, each lane a 16-B piece; fl_pieces turns them into this
+  // lane's two natural pieces (lanes l, l^8 trade one piece by DPP row_ror:8)
+  constexpr bool FL_LOAD = SIREN_FULLLINE && SN == 4 && !nt_is_fwd(MODE);
+  auto fl_load = [&](int mtop, int ncol, uint4 (&raw)[SN / 2]) {
+    const size_t ra = (size_t)(mtop + (lane & 7)) * N + ncol + ((lane & 8) ? 32 : 0);
+    raw[0] = *(const uint4*)(p.Cprev + ra);
+    raw[1] = *(const uint4*)(p.Cprev + ra + (size_t)8 * N);
+  };
+  auto fl_pieces = [&](const uint4 (&raw)[SN / 2], int pp) {
+    const bool hi = (lane & 8) != 0;
+    const uint4 send = hi ? raw[0] : raw[1];
+    uint4 recv;
+    recv.x = __builtin_amdgcn_update_dpp(0, (int)send.x, 0x128, 0xf, 0xf, false);
+    recv.y = __builtin_amdgcn_update_dpp(0, (int)send.y, 0x128, 0xf, 0xf, false);
+    recv.z = __builtin_amdgcn_update_dpp(0, (int)send.z, 0x128, 0xf, 0xf, false);
+    recv.w = __builtin_amdgcn_update_dpp(0, (int)send.w, 0x128, 0xf, 0xf, false);
+    return pp == 0 ? (hi ? recv : raw[0]) : (hi ? raw[1] : recv);
+  };
   auto pre = [&](int g) {
     int m0, n0;
     tile_of(g, m0, n0);
@@ -281,10 +300,15 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     const int mrow0 = m0 + wm * TM + (lane & 15);
     if constexpr (!nt_is_fwd(MODE)) {
 #pragma unroll
-      for (int j = 0; j < PRE_J; ++j)
+      for (int j = 0; j < PRE_J; ++j) {
+        if constexpr (FL_LOAD) {
+          fl_load(m0 + wm * TM + j * 16, npc, cp_in[j]);
+        } else {
 #pragma unroll
-        for (int pp = 0; pp < SN / 2; ++pp)
-          cp_in[j][pp] = *(const uint4*)(p.Cprev + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
+          for (int pp = 0; pp < SN / 2; ++pp)
+            cp_in[j][pp] = *(const uint4*)(p.Cprev + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
+        }
+      }
       if constexpr (nt_is_dx0(MODE)) {
 #pragma unroll
         for (int j = 0; j < SM; ++j) {
@@ -439,11 +463,21 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           t0 = t_in[j][0];
           t1 = t_in[j][1];
         }
+        uint4 fl_raw[SN / 2];
+        if constexpr (FL_LOAD) {
+          if (j < PRE_J) {
+            fl_raw[0] = cp_in[j < PRE_J ? j : 0][0];
+            fl_raw[1] = cp_in[j < PRE_J ? j : 0][1];
+          } else {
+            fl_load(m0 + wm * TM + j * 16, npc, fl_raw);
+          }
+        }
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
           uint2 cpu[2];
-          const uint4 cpv = (j < PRE_J) ? cp_in[j < PRE_J ? j : 0][pp]
-                                        : *(const uint4*)(p.Cprev + rowoff + npc + pp * 32);
+          uint4 cpv;
+          if constexpr (FL_LOAD) cpv = fl_pieces(fl_raw, pp);
+          else cpv = (j < PRE_J) ? cp_in[j < PRE_J ? j : 0][pp] : *(const uint4*)(p.Cprev + rowoff + npc + pp * 32);
           unswap16_pair(cpv, cpu[0], cpu[1]);
           uint2 epu[2];
           if constexpr (MODE == NT_DX_SNAKE || MODE == NT_DX0_SNAKE)
