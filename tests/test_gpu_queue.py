@@ -89,6 +89,39 @@ def test_queue_bit_identical_to_static_walk(lib, dev, R, H, grid):
     assert _same(_run_all(lib, dev, R, H, inp, st), ref)
 
 
+@pytest.mark.parametrize("act", ["snake", "tanh"])
+@pytest.mark.parametrize("grid", [8, 0])
+def test_queue_act_forward_bit_identical(lib, dev, act, grid):
+    """The Snake / Tanh forward epilogues (modes NT_FWD_SNAKE / NT_FWD_TANH, with and without the
+    head partials) from the queue == from the static walk."""
+    R, H = 4096, 512
+    code = {"snake": 1, "tanh": 2}[act]  # SIREN_ACT_SNAKE, SIREN_ACT_TANH
+    ok(lib.siren_set_option(0, 256), lib)
+    ok(lib.siren_set_option(2, 4), lib)
+    ok(lib.siren_set_option(4, grid), lib)
+    X, W, b, hw, *_ = _inputs(dev, R, H, seed=11)
+    a = 0.5 + torch.rand(H, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        res = []
+        for head in (False, True):
+            Y = torch.full((R, H), float("nan"), dtype=H16, device=dev)
+            C = torch.full_like(Y, float("nan"))
+            E = torch.full_like(Y, float("nan"))
+            hp = torch.full((H // 128, R), float("nan"), device=dev)
+            ok(lib.siren_inner_fwd_act(P(X), P(W), P(b), code, ctypes.c_float(1.0), P(a), R, H, P(Y), P(C),
+                                       P(E) if act == "snake" else 0, P(hw) if head else 0, P(hp) if head else 0,
+                                       s), lib)
+            torch.cuda.synchronize()
+            res += [Y, C] + ([E] if act == "snake" else []) + ([hp[:H // 256]] if head else [])
+        return res
+    ok(lib.siren_set_option(8, 0), lib)
+    ref = run()
+    ok(lib.siren_set_option(8, 1), lib)
+    assert _same(run(), ref)
+
+
 def test_queue_forward_vs_fp64(lib, dev):
     R, H = 4096, 512
     ok(lib.siren_set_option(0, 256), lib)
