@@ -42,6 +42,9 @@
 #ifndef SIREN_WPOL
 #define SIREN_WPOL 0  // ... of the W operand
 #endif
+#ifndef SIREN_STPOL
+#define SIREN_STPOL 0  // epilogue store cache policy (measurement builds; see st16)
+#endif
 #ifndef SIREN_FULLLINE
 #define SIREN_FULLLINE 0  // forward epilogue stores as whole 128-B lines (measurement builds)
 #endif
@@ -254,7 +257,16 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   float* red = (float*)(smem + Cfg::RING);
   // 16-B epilogue store; SIREN_OPT_NT_DIAG bit 1 (measurement only) keeps the value live
   // and drops the store
-  auto st16 = [&](h16* dst, uint4 v) { *(uint4*)dst = v; };
+  // SIREN_STPOL (measurement builds): cache policy of the epilogue's 16-B stores -- 0 plain,
+  // 1 nt, 2 sc1 (write-through), 3 sc0 sc1
+  auto st16 = [&](h16* dst, uint4 v) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    [[maybe_unused]] const u32x4 w = u32x4{v.x, v.y, v.z, v.w};
+    if constexpr (SIREN_STPOL == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(w) : "memory");
+    else if constexpr (SIREN_STPOL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(w) : "memory");
+    else if constexpr (SIREN_STPOL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(w) : "memory");
+    else *(uint4*)dst = v;
+  };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
   float* bias_lds = (float*)(smem + Lay::BIAS);
