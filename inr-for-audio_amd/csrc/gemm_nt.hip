@@ -32,6 +32,8 @@
 // and Cprev load is a 16-B row piece.  The epilogue's store tail is issue-bound (measured:
 // 64 scattered dwordx2 per lane cost 1.0 ms of a 2.8 ms forward GEMM), so halving the
 // instruction count and keeping the stores behind two prefetched stages is what matters.
+#include <mutex>
+
 #include "gemm_pipeline.h"
 #include "siren_common.h"
 #include "siren_kernels.h"
@@ -732,6 +734,8 @@ void gemm_nt_set_queue(int v) { g_nt_queue = v; }
 constexpr int kQueueSets = 16;
 __device__ int g_ntq[kQueueSets][kQueueSet];
 static int* nt_queue(hipStream_t s) {
+  static std::mutex mu;  // host threads that launch concurrently get distinct sets
+  std::lock_guard<std::mutex> lock(mu);
   static struct { int dev; hipStream_t s; } used[kQueueSets];
   static int nused = 0;
   static int* base[64] = {};

@@ -85,3 +85,19 @@ def test_supported_hidden_sizes_validate(lib, hidden):
     # only shape checks run (NULL outputs make it return before any launch)
     assert lib.siren_head_bwd(None, None, None, None, ctypes.c_float(30), 128, hidden, None, None, None,
                               None, None, None, None) == 1002
+
+
+def test_set_option_ranges(lib):
+    """siren_set_option validates every knob on the host (SIREN_OPT_* in siren_hip.h) and leaves
+    the defaults restored; SIREN_OPT_NT_QUEUE takes 0 (static walk), 1 (forward modes), 2 (all)."""
+    bad = 1003  # SIREN_ERR_CONFIG
+    for opt, good, wrong in ((0, (0, 128, 256), (64,)), (1, (0, 128, 256), (512,)), (2, (-1, 0, 7), (8, -2)),
+                             (3, (-1, 4), (5,)), (4, (0, 16), (-1,)), (5, (0, 64), (65,)),
+                             (6, (0, 1, 4, 512, 1024), (2, 8)), (7, (1, 16), (0, 17)), (8, (0, 1, 2), (3, -1))):
+        for v in good:
+            assert lib.siren_set_option(opt, v) == 0, (opt, v)
+        for v in wrong:
+            assert lib.siren_set_option(opt, v) == bad, (opt, v)
+    assert lib.siren_set_option(99, 0) == bad
+    for opt, v in ((0, 0), (1, 0), (2, -1), (3, -1), (4, 0), (5, 0), (6, 0), (7, 2), (8, 1)):
+        assert lib.siren_set_option(opt, v) == 0
