@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--queue", default="0,1")
     ap.add_argument("--cases", default="fwd,dx")
     ap.add_argument("--grid", type=int, default=0, help="SIREN_OPT_NT_GRID (0 = one block per CU)")
+    ap.add_argument("--diags", default="0", help="SIREN_OPT_NT_DIAG values (timing-only ablations; the "
+                    "queue is off while one is set)")
     args = ap.parse_args()
     import __graft_entry__ as ge
     path = ge.build_diagnostic(["SIREN_NT_STAMPS"], "libsiren_hip_stamps.so")
@@ -103,8 +105,9 @@ def main():
     out = {}
     for name in args.cases.split(","):
         for q in [int(x) for x in args.queue.split(",")]:
-            for stg in [int(x) for x in args.staggers.split(",")]:
+            for stg, dg in [(int(x), int(d)) for x in args.staggers.split(",") for d in args.diags.split(",")]:
                 _lib.check(lib.siren_set_option(8, 2 if q else 0), "queue")
+                _lib.check(lib.siren_set_option(6, dg), "diag")
                 _lib.check(lib.siren_set_option(5, stg), "stagger")
                 _lib.check(lib.siren_set_option(4, args.grid), "grid")
                 for _ in range(3):
@@ -119,10 +122,11 @@ def main():
                 lib.siren_debug_nt_stamps(None)
                 st = buf.cpu().numpy().view(np.uint64).reshape(ncu, 256, 4)
                 r = analyse(st, ev0.elapsed_time(ev1))
-                key = f"{name}_q{q}_s{stg}"
+                key = f"{name}_q{q}_s{stg}_d{dg}"
                 out[key] = r
                 print(key, json.dumps(r), flush=True)
     lib.siren_set_option(5, 0)
+    lib.siren_set_option(6, 0)
     lib.siren_set_option(8, 1)
 
 
