@@ -260,13 +260,15 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // 16-B epilogue store; SIREN_OPT_NT_DIAG bit 1 (measurement only) keeps the value live
   // and drops the store
   // SIREN_STPOL (measurement builds): cache policy of the epilogue's 16-B stores -- 0 plain,
-  // 1 nt, 2 sc1 (write-through), 3 sc0 sc1
+  // 1 nt, 2 sc1 (write-through), 3 sc0 sc1.  The asm forms carry their own s_nop: hipcc's hazard
+  // recognizer does not see that a VALU write of the data VGPRs must wait a cycle after a
+  // 128-bit store (without it the outputs differed from the plain build's)
   auto st16 = [&](h16* dst, uint4 v) {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     [[maybe_unused]] const u32x4 w = u32x4{v.x, v.y, v.z, v.w};
-    if constexpr (SIREN_STPOL == 1) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(w) : "memory");
-    else if constexpr (SIREN_STPOL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(w) : "memory");
-    else if constexpr (SIREN_STPOL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(w) : "memory");
+    if constexpr (SIREN_STPOL == 1) asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(dst), "v"(w) : "memory");
+    else if constexpr (SIREN_STPOL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(w) : "memory");
+    else if constexpr (SIREN_STPOL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(dst), "v"(w) : "memory");
     else *(uint4*)dst = v;
   };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
@@ -681,10 +683,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #ifdef SIREN_NT_STAMPS
       if (p.stamps) {
         const unsigned long long st_e = rt_now();
+        unsigned long long cyc;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(cyc)::"memory");
         if (tid == 0 && ti < 256) {
           unsigned long long* sp = p.stamps + ((size_t)blockIdx.x * 256 + ti) * 4;
           sp[0] = st_prev;
-          sp[1] = (unsigned long long)g_cur;
+          sp[1] = cyc;  // shader-clock counter at st_e: the clock between two tiles
           sp[2] = st_m;
           sp[3] = st_e;
         }

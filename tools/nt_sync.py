@@ -29,7 +29,8 @@ sys.path.insert(0, ROOT)
 
 
 def analyse(st, ms):
-    """st [grid][256][4] u64 (10 ns ticks; unused slots 0)."""
+    """st [grid][256][4] u64: {start, shader-clock count, end of MFMAs, end of epilogue}, times in
+    10 ns ticks (unused slots 0)."""
     rows = []
     for b in range(st.shape[0]):
         for i in range(st.shape[1]):
@@ -57,13 +58,17 @@ def analyse(st, ms):
     first = start[ti == 0]
     conc_early = float(np.median(conc[ti <= 2]))
     conc_late = float(np.median(conc[ti >= 10]))
-    # epilogue-start phase of each block's tiles 10.. relative to block 0's tile period
     per = float(np.median(te[ti >= 1] - start[ti >= 1]))
+    # shader clock between consecutive tiles of a block: d(s_memtime) / d(real time)
+    cyc = a[:, 3]
+    same = a[1:, 0] == a[:-1, 0]
+    dcyc, dt = (cyc[1:] - cyc[:-1])[same], (te[1:] - te[:-1])[same]
+    clk = float(np.median(dcyc / np.maximum(dt, 1e-3)) / 1e3)  # cycles per us / 1e3 = GHz
     return {"ms": ms, "tiles": len(a), "main_us": float(np.median(main)), "epi_us": float(np.median(epi)),
             "conc_med": float(np.median(conc)), "epi_by_conc": by,
             "burst": float(h.max() / max(h.mean(), 1e-9)), "span_us": float(te.max()),
             "first_start_spread_us": float(first.max() - first.min()), "conc_tiles_0_2": conc_early,
-            "conc_tiles_10plus": conc_late, "tile_period_us": per}
+            "conc_tiles_10plus": conc_late, "tile_period_us": per, "clock_ghz": clk}
 
 
 def main():
