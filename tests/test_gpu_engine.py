@@ -121,6 +121,25 @@ def test_graph_replay_matches_eager(dev):
     assert np.array_equal(la, lb)
 
 
+def test_graph_replay_with_tile_queue(dev, lib):
+    """At 65 536 rows x 512 the forward GEMMs take the 256-tile ping-pong kernel with the dynamic
+    tile queue (256 tiles, grid % 8 == 0): a captured step replays the queue kernels (their
+    counters re-zero themselves at the end of every launch) and stays bit-identical to eager."""
+    from inr_for_audio_amd.engine import SirenEngine
+    assert lib.siren_nt_tile(65536, 512) == 256
+    t, y = _signal(65536)
+    a = SirenEngine(_model(512, 2, 2000.0), t, y, device=dev)
+    b = SirenEngine(_model(512, 2, 2000.0), t, y, device=dev)
+    for _ in range(4):
+        a.step()
+    b.step()
+    b.capture_graph()
+    for _ in range(3):
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params)
+
+
 def test_determinism(dev):
     from inr_for_audio_amd.engine import SirenEngine
     t, y = _signal(3000)
