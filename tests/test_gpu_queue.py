@@ -72,7 +72,9 @@ def _same(a, b):
 
 
 @pytest.mark.parametrize("R,H,grid", [(4096, 1024, 8), (4096, 1024, 16), (4096, 1024, 24), (4096, 1024, 0),
-                                      (3072, 512, 8), (6144, 256, 16)])
+                                      (3072, 512, 8), (6144, 256, 16),
+                                      # 20 tiles: shards of 2 and 3 tiles (uneven eighths)
+                                      (2560, 512, 8), (2560, 512, 16)])
 def test_queue_bit_identical_to_static_walk(lib, dev, R, H, grid):
     ok(lib.siren_set_option(0, 256), lib)
     ok(lib.siren_set_option(2, 4), lib)
