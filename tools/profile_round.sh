@@ -4,6 +4,7 @@
 #   trace/                  rocprofv3 --kernel-trace --stats of a short bench run
 #   bench_pmc_hbm.json      FETCH_SIZE and WRITE_SIZE, each in its own --pmc pass
 #   bench_pmc_mfma.json     SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE: MFMA utilisation per kernel
+#   bench_pmc_lds.json      SQ_LDS_IDX_ACTIVE / _BANK_CONFLICT / _UNALIGNED_STALL + GRBM_GUI_ACTIVE
 #   bench_cfg{3,4,5}.json   the other BASELINE configs' bench lines; trace_cfg{3,4,5}/ their
 #                           rocprofv3 --kernel-trace --stats
 # Every GPU step has its own time limit and the steps are chained with &&.
@@ -24,6 +25,9 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_wr
   python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mfma" -o run -- \
   python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_mfma.log" 2>&1 &&
+timeout -k 10 400 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_lds" -o run -- \
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_lds.log" 2>&1 &&
+python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_lds.json" "$OUT/pmc_lds" &&
 python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_hbm.json" "$OUT/pmc_fetch" "$OUT/pmc_write" &&
 python3 "$ROOT/tools/pmc_mfma.py" "$OUT/bench_pmc_mfma.json" "$OUT/pmc_mfma" &&
 for c in cfg3 cfg4 cfg5; do
