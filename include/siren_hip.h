@@ -26,9 +26,15 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 7
+#define SIREN_ABI_VERSION 8
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
+/* ints in one tile-queue counter set (siren_batch.tileq, siren_inner_fwd's tileq): the
+ * hidden-layer forward GEMM's persistent blocks pull their tiles from it.  Caller-owned device
+ * memory, any content: the library zeroes it on the stream before every launch that uses it.
+ * One set serves every launch of one stream in order; launches that may run concurrently
+ * (other streams, other devices, replays of other captured graphs) need sets of their own. */
+#define SIREN_TILEQ_INTS 768
 
 enum siren_status {
   SIREN_OK = 0,
@@ -148,6 +154,8 @@ typedef struct siren_batch {
    * ('mae': sse slot = sum |err|, g = sign(err) / n_total) */
   int32_t loss_mode, pad1;
   const siren_guard* guard;  /* range guard (NULL: fixed headroom 6, no overflow recovery) */
+  int32_t* tileq;            /* SIREN_TILEQ_INTS ints of tile-queue counters on the device of the
+                                activations (NULL: the forward GEMM's static tile walk) */
 } siren_batch;
 
 /* Workspace sizing / tiling helpers.  siren_nt_tile: tile edge the NT GEMMs use for
@@ -194,17 +202,18 @@ int siren_coords_fill_grid(float* xy, int64_t rows, int64_t offset, int64_t heig
 int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float* b0, float omega0,
                     int32_t rows, int32_t hidden, uint16_t* Y0, uint16_t* C0, void* stream);
 /* models.py:114-115 hidden SineLayer: Y = sin(omega(X W^T + b)), C = cos(.); optional head
- * partial dot (models.py:374-381) when head_w != NULL */
+ * partial dot (models.py:374-381) when head_w != NULL; tileq: SIREN_TILEQ_INTS ints for the
+ * dynamic tile queue (NULL: static tile walk; results are identical) */
 int siren_inner_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, float omega, int32_t rows,
                     int32_t hidden, uint16_t* Y, uint16_t* C, const float* head_w, float* head_part,
-                    void* stream);
+                    int32_t* tileq, void* stream);
 /* any inner layer kind: SINE as siren_inner_fwd; SNAKE (models.py:235-241): z = X W^T + b,
  * Y = z + sin^2(a z)/a, C = 1 + sin(2az), E = (z sin(2az) - sin^2(az)/a)/a; TANH
  * (models.py:366-372): Y = tanh z, C = 1 - Y^2 (a, E unused) */
 int siren_inner_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, int32_t act,
                         float omega, const float* a, int32_t rows, int32_t hidden, uint16_t* Y,
                         uint16_t* C, uint16_t* E, const float* head_w, float* head_part,
-                        void* stream);
+                        int32_t* tileq, void* stream);
 /* run.py:125,168 MSELoss + final Linear bias: out, g = 2(out-y)/n_total, partial sums
  * (gmax_part may be NULL); the L1Loss of loss_mode 1 is reached through siren_train_step */
 int siren_head_loss(const float* head_part, int32_t nparts, int32_t rows, const float* b_head,
@@ -340,32 +349,27 @@ enum siren_prof_kind {
 };
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
  * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;
- * SIREN_OPT_NT_PIPE = 256x256 NT GEMM variant: -1 automatic (4, every mode; the Snake / Tanh
- * modes take 4 or else 1), 0 BK 64 one tile per block, 1 BK 64 persistent, 2 BK 32 4-slot ring persistent, 3 BK 32 3-slot ring persistent,
- * 4 BK 64 persistent with two wave groups in ping-pong, 5 BK 64 persistent with the X operand
- * prefetched into L2 SIREN_OPT_NT_PF_DIST (1..16, default 2) K-steps ahead, 6 / 7 128x256 tiles
- * (4 waves), BK 32 3- / 2-slot ring, persistent with two blocks per CU;
+ * SIREN_OPT_NT_PIPE = 256x256 NT GEMM K-loop: -1 automatic (4), 0 BK 64 one tile per block,
+ * 1 BK 64 persistent double buffer, 4 BK 64 persistent with two wave groups in ping-pong;
  * SIREN_OPT_TN_PIPE = -1..4 selects the 256x256 dW K-loop (-1 automatic = 4; 0: BK 64 double
  * buffer, 1: BK 32 4-slot ring, 2: BK 32 5-slot ring, 3: BK 64 ping-pong in 16-MFMA phases,
  * 4: BK 64 ping-pong in 32-MFMA segments);
  * SIREN_OPT_NT_GRID = persistent NT grid size (0 = one block per CU; tests use small
  * values so every block walks several tiles);
- * SIREN_OPT_NT_DIAG = measurement-only NT ablations (results are WRONG while set): bit 0 reads
- *   the X operand from the first 4 row bands only (L2-resident operand); ping-pong K-loop
- *   (pipe 4) only: bit 2 reads W from column tile 0 only (L2-resident W), bit 9 runs no tiles,
- *   bit 10 skips the epilogue (its compute and stores).
- *   (The r05 bits 1-3 -- no stores, identity sin/cos, non-temporal stores -- were retired in r06: their
- *   per-store branches cost the production epilogue; DESIGN.md keeps their measurements);
- * SIREN_OPT_NT_STAGGER = persistent NT start stagger: block b idles (b % 16) * value units of
- * ~1.7k cycles before its first tile, so that the blocks' epilogue store bursts do not
- * coincide (0 = none; 0..64);
+ * SIREN_OPT_NT_DIAG = measurement-only NT ablations, accepted only by libraries built with
+ *   -DSIREN_DIAG (__graft_entry__.build_diagnostic; the product library returns
+ *   SIREN_ERR_CONFIG for any non-zero value); results are WRONG while set: bit 0 reads the X
+ *   operand from the first 4 row bands only (L2-resident operand); ping-pong K-loop only: bit 2
+ *   reads W from column tile 0 only (L2-resident W), bit 9 runs no tiles, bit 10 skips the
+ *   epilogue (its compute and stores);
  * SIREN_OPT_NT_QUEUE = 1 (default): the ping-pong NT GEMM's persistent blocks take their tiles
- * from a per-stream dynamic queue (8 shard heads, agent-scope atomics) in the forward modes,
- * 2: in every mode, 0: never (the static walk b, b + G, ...).  Results are identical. */
+ * from the caller's tile-queue set (siren_batch.tileq; 8 shard heads, agent-scope atomics) in the
+ * forward modes, 2: in every mode, 0: never (the static walk b, b + G, ...).  Results are
+ * identical.  (Options 5 and 7, the round-2 start stagger and X L2-prefetch distance, were
+ * measured neutral or slower and retired with their kernels: they return SIREN_ERR_CONFIG.) */
 enum siren_option {
   SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1, SIREN_OPT_NT_PIPE = 2, SIREN_OPT_TN_PIPE = 3,
-  SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_STAGGER = 5, SIREN_OPT_NT_DIAG = 6,
-  SIREN_OPT_NT_PF_DIST = 7, SIREN_OPT_NT_QUEUE = 8
+  SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_DIAG = 6, SIREN_OPT_NT_QUEUE = 8
 };
 int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);

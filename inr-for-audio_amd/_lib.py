@@ -13,9 +13,10 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 MAX_INNER = 16
 ROW_TILE = 128
+TILEQ_INTS = 768  # SIREN_TILEQ_INTS: one tile-queue counter set
 ACT_SINE, ACT_SNAKE, ACT_TANH = 0, 1, 2  # siren_act
 FP32_IDENTITY, FP32_SIN, FP32_TANH, FP32_SNAKE = 0, 1, 2, 3  # siren_fp32_act
 
@@ -78,7 +79,7 @@ class SirenBatch(ctypes.Structure):
         ("gmax_part", _p), ("gscale", _p), ("col_part", _p), ("col_part2", _p), ("red_tmp", _p), ("slab", _p),
         ("E", _p * (MAX_INNER + 1)),
         ("grad_ready", _p * (MAX_INNER + 2)),
-        ("loss_mode", _i32), ("pad1", _i32), ("guard", _p),
+        ("loss_mode", _i32), ("pad1", _i32), ("guard", _p), ("tileq", _p),
     ]
 
 
@@ -126,12 +127,12 @@ _SIGS = {
     "siren_coords_fill": (ctypes.c_int, [_p, _i64, _i64, _i64, _p]),
     "siren_coords_fill_grid": (ctypes.c_int, [_p, _i64, _i64, _i64, _i32, _p]),
     "siren_first_fwd": (ctypes.c_int, [_p, _i32, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p]),
-    "siren_inner_fwd": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p]),
+    "siren_inner_fwd": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p, _p]),
     "siren_head_loss": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _i32, ctypes.c_double, _p, _p, _p, _p,
                                        _p, _p]),
     "siren_grad_scale": (ctypes.c_int, [_p, _i32, _p, _i32, ctypes.c_float, _p, _p]),
     "siren_inner_fwd_act": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_float, _p, _i32, _i32, _p, _p, _p, _p,
-                                           _p, _p]),
+                                           _p, _p, _p]),
     "siren_head_bwd": (ctypes.c_int, [_p, _p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, _p, _p, _p, _p,
                                       _p]),
     "siren_inner_bwd_dx_act": (ctypes.c_int, [_p, _p, _p, _p, _i32, ctypes.c_float, _i32, _i32, _p, _p, _p,
@@ -192,6 +193,13 @@ def load(path: str = LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    _lib = bind(path)
+    return _lib
+
+
+def bind(path: str):
+    """A freshly bound (uncached) handle of the library at `path`: tools/ab_bench.py loads the
+    product library beside measurement builds of it under other file names."""
     if not os.path.exists(path):
         raise SirenError(
             f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
@@ -206,7 +214,6 @@ def load(path: str = LIB_PATH):
     for k, st in enumerate(STRUCTS):
         if lib.siren_struct_size(k) != ctypes.sizeof(st):
             raise SirenError(f"{st.__name__}: ctypes size {ctypes.sizeof(st)} != C size {lib.siren_struct_size(k)}")
-    _lib = lib
     return lib
 
 
@@ -224,3 +231,9 @@ def ptr(t) -> int:
 
 def stream_handle(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def new_tileq(device) -> torch.Tensor:
+    """A tile-queue counter set (SIREN_TILEQ_INTS int32 on `device`; the library zeroes it before
+    each launch that uses it).  One per stream of concurrent launches."""
+    return torch.zeros(TILEQ_INTS, dtype=torch.int32, device=device)

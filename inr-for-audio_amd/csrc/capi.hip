@@ -9,6 +9,7 @@ using namespace siren;
 
 static_assert(sizeof(siren_opt_state) == sizeof(OptState), "opt state layout");
 static_assert(sizeof(siren_guard) == sizeof(GuardState), "guard layout");
+static_assert(SIREN_TILEQ_INTS == kTileqInts, "tile-queue set size");
 static_assert((int)SIREN_FP32_SNAKE == (int)siren::FP32_SNAKE && (int)SIREN_FP32_SIN == (int)siren::FP32_SIN &&
                   (int)SIREN_FP32_TANH == (int)siren::FP32_TANH, "fp32 act codes");
 
@@ -130,6 +131,7 @@ hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s) {
     const bool head = (i == L - 1);
     p.head_w = n->w_head;
     p.head_part = b->head_part;
+    p.tileq = b->tileq;
     SIREN_PROF(SIREN_PROF_INNER_FWD, s, gemm_nt(fwd_mode(n->act[i]), head, p, s));
   }
   return hipSuccess;
@@ -251,6 +253,7 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
     p.tile = ntile;
     p.colsum_part = b->col_part;
     p.gscale = b->gscale;
+    p.tileq = b->tileq;  // used only with SIREN_OPT_NT_QUEUE 2
     if (i > 0) {
       const bool snake = net->act[i - 1] == SIREN_ACT_SNAKE;
       p.omega = act_omega(net, i - 1);
@@ -374,7 +377,7 @@ int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float
 
 int siren_inner_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, float omega, int32_t rows,
                     int32_t hidden, uint16_t* Y, uint16_t* C, const float* head_w, float* head_part,
-                    void* stream) {
+                    int32_t* tileq, void* stream) {
   if (!X || !Wh || !b || !Y || !C) return SIREN_ERR_NULL;
   if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
   if (head_w && !head_part) return SIREN_ERR_NULL;
@@ -382,7 +385,7 @@ int siren_inner_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, float
   p.X = B(X); p.W = B(Wh); p.M = rows; p.N = hidden; p.K = hidden;
   p.tile = nt_choose_tile(rows, hidden);
   p.omega = omega; p.bias = b; p.Y = B(Y); p.C = B(C);
-  p.head_w = head_w; p.head_part = head_part;
+  p.head_w = head_w; p.head_part = head_part; p.tileq = tileq;
   return (int)gemm_nt(NT_FWD, head_w != nullptr, p, S(stream));
 }
 
@@ -416,7 +419,7 @@ int siren_head_bwd(const uint16_t* C, const uint16_t* Y, const float* g, const f
 int siren_inner_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, int32_t act,
                         float omega, const float* a, int32_t rows, int32_t hidden, uint16_t* Y,
                         uint16_t* C, uint16_t* E, const float* head_w, float* head_part,
-                        void* stream) {
+                        int32_t* tileq, void* stream) {
   if (!X || !Wh || !b || !Y || !C) return SIREN_ERR_NULL;
   if (act < SIREN_ACT_SINE || act > SIREN_ACT_TANH) return SIREN_ERR_CONFIG;
   if (act == SIREN_ACT_SNAKE && (!a || !E)) return SIREN_ERR_NULL;
@@ -426,7 +429,7 @@ int siren_inner_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, i
   p.X = B(X); p.W = B(Wh); p.M = rows; p.N = hidden; p.K = hidden;
   p.tile = nt_choose_tile(rows, hidden);
   p.omega = omega; p.bias = b; p.Y = B(Y); p.C = B(C); p.E = B(E); p.act_a = a;
-  p.head_w = head_w; p.head_part = head_part;
+  p.head_w = head_w; p.head_part = head_part; p.tileq = tileq;
   return (int)gemm_nt(fwd_mode(act), head_w != nullptr, p, S(stream));
 }
 
@@ -568,28 +571,20 @@ int siren_set_option(int32_t option, int32_t value) {
       else gemm_tn_set_tile(value);
       return SIREN_OK;
     case SIREN_OPT_NT_PIPE:
+      if (value != -1 && value != 0 && value != 1 && value != 4) return SIREN_ERR_CONFIG;
+      gemm_nt_set_pipe(value);
+      return SIREN_OK;
     case SIREN_OPT_TN_PIPE:
-      if (value < -1 || value > (option == SIREN_OPT_NT_PIPE ? 7 : 4))
-        return SIREN_ERR_CONFIG;
-      if (option == SIREN_OPT_NT_PIPE) gemm_nt_set_pipe(value);
-      else gemm_tn_set_pipe(value);
+      if (value < -1 || value > 4) return SIREN_ERR_CONFIG;
+      gemm_tn_set_pipe(value);
       return SIREN_OK;
     case SIREN_OPT_NT_GRID:
       if (value < 0) return SIREN_ERR_CONFIG;
       gemm_nt_set_grid_cap(value);
       return SIREN_OK;
-    case SIREN_OPT_NT_PF_DIST:
-      if (value < 1 || value > 16) return SIREN_ERR_CONFIG;
-      gemm_nt_set_pf_dist(value);
-      return SIREN_OK;
     case SIREN_OPT_NT_DIAG:
       if (value < 0 || (value & ~(1 | 4 | 512 | 1024))) return SIREN_ERR_CONFIG;
-      gemm_nt_set_diag(value);
-      return SIREN_OK;
-    case SIREN_OPT_NT_STAGGER:
-      if (value < 0 || value > 64) return SIREN_ERR_CONFIG;
-      gemm_nt_set_stagger(value);
-      return SIREN_OK;
+      return gemm_nt_set_diag(value) ? SIREN_OK : SIREN_ERR_CONFIG;
     case SIREN_OPT_NT_QUEUE:
       if (value < 0 || value > 2) return SIREN_ERR_CONFIG;
       gemm_nt_set_queue(value);

@@ -132,56 +132,33 @@ __device__ __forceinline__ void lds_barrier() {
 //   epi(tile)              consumes acc; the ring is NOT available to it (own LDS scratch;
 //                          raw barriers only -- every wave calls epi the same number of times).
 // SLACK = vector-memory instructions every wave's epilogue issues (a lower bound; 0 is always
-// safe).  G = vector-memory instructions per wave per stage, the last PF of which are L2
-// prefetches of a LATER stage's operand: a stage's wait lets its own PF prefetches stay in
-// flight, so each prefetch has two K-steps to land (in-order vmcnt), and the LDS-DMA it
-// runs ahead of then hits L2.
-// SIREN_NT_STAMPS (diagnostic builds only, tools/nt_stamps.py): thread 0 of each block
-// records per tile {start, cycles in K-step waits+barriers, end of MFMAs, end of epilogue}
-// with s_memtime into stamps[block][tile][4].
-#ifdef SIREN_NT_STAMPS
-__device__ __forceinline__ unsigned long long stamp_now() {
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-#endif
+// safe); G = vector-memory instructions per wave per stage.
 
-// s_waitcnt vmcnt(G*y + PF + (relaxed ? SLACK : 0)) for a wave-uniform y in [0, J]
-// (PF: the stage's own trailing L2-prefetch instructions, which may stay in flight)
-template <int G, int SLACK, int J, int PF = 0>
+// s_waitcnt vmcnt(G*y + (relaxed ? SLACK : 0)) for a wave-uniform y in [0, J]
+template <int G, int SLACK, int J>
 __device__ __forceinline__ void wait_stage(int y, bool relaxed) {
   if constexpr (J >= 0) {
     if (y == J) {
-      if (relaxed) wait_vmcnt<G * J + PF + SLACK>();
-      else wait_vmcnt<G * J + PF>();
+      if (relaxed) wait_vmcnt<G * J + SLACK>();
+      else wait_vmcnt<G * J>();
       return;
     }
-    wait_stage<G, SLACK, J - 1, PF>(y, relaxed);
+    wait_stage<G, SLACK, J - 1>(y, relaxed);
   } else {
     wait_vmcnt<0>();
   }
 }
 
-template <int S, int KK, int G, int NA, int NB, int SLACK, int PF, class StageFn, class FragFn,
-          class PreFn, class EpiFn>
+template <int S, int KK, int G, int NA, int NB, int SLACK, class StageFn, class FragFn, class PreFn,
+          class EpiFn>
 __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&acc)[NA][NB],
                                                     StageFn&& stage, FragFn&& frags, PreFn&& pre,
-                                                    EpiFn&& epi,
-                                                    unsigned long long* stamps = nullptr) {
+                                                    EpiFn&& epi) {
   static_assert(S >= 2 && S <= 6, "ring depth");
   constexpr int YMAX = (S == 2) ? 1 : S - 2;  // younger stages in flight at a wait
-  static_assert(SLACK >= 0 && PF >= 0 && PF <= G && G * YMAX + PF + SLACK < 64, "vmcnt immediate");
+  static_assert(SLACK >= 0 && G * YMAX + SLACK < 64, "vmcnt immediate");
   const int total = ntiles * nk;
   if (total <= 0) return;
-#ifdef SIREN_NT_STAMPS
-  unsigned long long st_tile = 0, st_wait = 0, st_a = 0;
-  stamps = stamps ? stamps + (size_t)blockIdx.x * 256 * 4 : nullptr;
-  const bool st_on = stamps && threadIdx.x == 0;
-#define SIREN_STAMP(x) x
-#else
-#define SIREN_STAMP(x)
-#endif
   int it = 0, ik = 0;  // issue pointer (tile, K-step)
   int issued = 0;      // stages issued so far (global step index of the next one)
   int fill = 0;        // ring slot of the next stage
@@ -197,11 +174,9 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
   int ct = 0, ck = 0, slot = 0;
   int relax = 0;  // K-steps left whose stage was issued before the last epilogue's stores
   for (int u = 0; u < total; ++u) {
-    SIREN_STAMP(st_a = stamp_now(); if (ck == 0) { st_tile = st_a; st_wait = 0; })
-    wait_stage<G, SLACK, YMAX, PF>(issued - (u + 1), relax > 0);
+    wait_stage<G, SLACK, YMAX>(issued - (u + 1), relax > 0);
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
-    SIREN_STAMP(st_wait += stamp_now() - st_a;)
     if (relax > 0) --relax;
     // stage u+S-1 goes into the slot K-step u-1 read (every wave is past the barrier)
     if (issued < total && issued < u + S) issue();
@@ -218,7 +193,6 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
     }
     __builtin_amdgcn_s_setprio(0);
     if (++ck == nk) {
-      SIREN_STAMP(const unsigned long long st_c = stamp_now();)
       pre(ct);
       if (S == 2 && issued == u + 2 && issued < total) {
         lds_barrier();  // every wave is done reading `slot` (== fill)
@@ -226,13 +200,6 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
       }
       relax = issued - (u + 1);  // stages in flight ahead of the stores
       epi(ct);
-      SIREN_STAMP(if (st_on && ct < 256) {
-        const unsigned long long st_d = stamp_now();
-        stamps[ct * 4 + 0] = st_tile;
-        stamps[ct * 4 + 1] = st_wait;
-        stamps[ct * 4 + 2] = st_c;
-        stamps[ct * 4 + 3] = st_d;
-      })
 #pragma unroll
       for (int i = 0; i < NA; ++i)
 #pragma unroll
@@ -245,7 +212,6 @@ __device__ __forceinline__ void mfma_pipeline_tiles(int ntiles, int nk, f32x4 (&
   wait_vmcnt<0>();
   wait_lgkm0();
   __builtin_amdgcn_s_barrier();
-#undef SIREN_STAMP
 }
 
 // ---- Ping-pong K-loop of the 256x256 / 8-wave GEMMs ----------------------------------------

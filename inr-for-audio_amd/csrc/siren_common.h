@@ -57,39 +57,18 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_byte) 
       : "memory");
 }
 
-// The same with an explicit cache policy on the load (POL: 0 default, 1 nt, 2 sc1, 3 sc0 sc1):
-// measurement hooks for the operand streams of the NT GEMM (SIREN_XPOL / SIREN_WPOL builds).
-template <int POL>
-__device__ __forceinline__ void glds16_asm_pol(const void* gsrc, unsigned lds_byte) {
-  if constexpr (POL == 0) {
-    glds16_asm(gsrc, lds_byte);
-  } else {
-    unsigned keep;
-    if constexpr (POL == 1)
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte)) : "memory");
-    else if constexpr (POL == 2)
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte)) : "memory");
-    else
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc0 sc1\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte)) : "memory");
-  }
-}
-
-// L2 prefetch: a 4-B LDS-DMA per lane (one touch per 128-B line) into a dummy 256-B LDS
-// area.  LDS-DMA rather than a load to a VGPR, whose late return would clobber a register
-// the compiler has already reused.  Counted by vmcnt like every other vector-memory op.
-__device__ __forceinline__ void gpf4_asm(const void* gsrc, unsigned lds_byte) {
+// The same in the saddr form: wave-uniform 64-bit base in SGPRs plus a 32-bit per-lane byte
+// offset, so that one VGPR of lane offset serves every piece whose lane pattern repeats.
+__device__ __forceinline__ void glds16_asm_s(unsigned voff, const void* sbase, unsigned lds_byte) {
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
+      "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dword %1, off\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte))
+      : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds_byte))
       : "memory");
 }
 

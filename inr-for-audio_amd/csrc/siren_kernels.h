@@ -41,25 +41,21 @@ struct NtParams {
   int in_dim;
   const float* gscale;  // NT_DX / NT_DX0: {S, 1/S} -- column partials are multiplied by 1/S
                         // (null = unscaled)
-  int pf_dist;          // NT_PIPE 5: X L2-prefetch distance in K-steps
-  int diag;             // SIREN_OPT_NT_DIAG ablation bits (0 in production)
-  int stagger;          // persistent grid: block b idles (b % 16) * stagger * ~1.7k cycles first
-  unsigned long long* stamps;  // SIREN_NT_STAMPS diagnostic builds only
-  // ping-pong K-loop only: dynamic tile queue (null = static walk b, b + G, ...).  8 shard heads
-  // and one done counter, 128 B apart, zero at launch; the last block to finish re-zeroes them
+  int diag;             // SIREN_OPT_NT_DIAG ablation bits (SIREN_DIAG measurement builds only)
+  // ping-pong K-loop only: caller-owned tile-queue counter set of kTileqInts ints (null = the
+  // static walk b, b + G, ...); gemm_nt zeroes it on the stream before each queue launch
   int* tileq;
 };
+constexpr int kTileqInts = 768;  // == SIREN_TILEQ_INTS (include/siren_hip.h)
 
 int nt_choose_tile(int M, int N);
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s);
 void gemm_nt_set_tile(int tile);  // 0 = auto, 128, 256 (A/B measurement)
 void gemm_tn_set_tile(int tile);
-void gemm_nt_set_pipe(int v);     // 1 = persistent 256x256 (default), 0 = one tile per block
+void gemm_nt_set_pipe(int v);     // 256x256 K-loop: 4 ping-pong (default), 1 persistent, 0 one tile per block
 void gemm_tn_set_pipe(int v);     // 256x256 K-loop variant (TnL0..TnL2)
 void gemm_nt_set_grid_cap(int cap);  // persistent grid size override (0 = #CUs)
-void gemm_nt_set_pf_dist(int d);   // SIREN_OPT_NT_PF_DIST
-void gemm_nt_set_diag(int bits);     // SIREN_OPT_NT_DIAG (measurement-only ablations)
-void gemm_nt_set_stagger(int units); // persistent grid start stagger (see NtParams::stagger)
+bool gemm_nt_set_diag(int bits);     // SIREN_OPT_NT_DIAG (false: not a SIREN_DIAG build)
 void gemm_nt_set_queue(int on);       // SIREN_OPT_NT_QUEUE: dynamic tile queue (ping-pong K-loop)
 struct TnParams {
   const h16* Y;   // [R][Hin]   layer input (A role: dW column index k)

@@ -121,6 +121,8 @@ class Workspace:
         self.gsum_part = e(nsum)
         self.gmax_part = e(nsum)
         self.gscale = torch.ones(2, dtype=f32, device=device)
+        # this workspace's tile-queue counters: its launches are ordered on one stream
+        self.tileq = _lib.new_tileq(device)
         self.train = train
         if train:
             self.splits = int(splits or lib.siren_default_splits(R, H))
@@ -153,6 +155,7 @@ class Workspace:
         b.gmax_part, b.gscale = ptr(self.gmax_part), ptr(self.gscale)
         b.col_part, b.col_part2 = ptr(self.col_part), ptr(self.col_part2)
         b.red_tmp, b.slab = ptr(self.red_tmp), ptr(self.slab)
+        b.tileq = ptr(self.tileq)
         return b
 
 

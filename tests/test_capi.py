@@ -44,7 +44,7 @@ def test_struct_layouts_match(lib):
 
 
 def test_host_only_helpers(lib):
-    assert lib.siren_abi_version() == 7
+    assert lib.siren_abi_version() == 8
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256
@@ -65,7 +65,7 @@ def test_validation_without_device(lib):
     net.in_dim, net.hidden = 1, 384
     assert lib.siren_forward(ctypes.byref(net), ctypes.byref(SirenBatch()), None) == 1001
     assert lib.siren_inner_fwd(None, None, None, ctypes.c_float(30), 128, 256, None, None, None, None,
-                               None) == 1002
+                               None, None) == 1002
     assert lib.siren_inner_bwd_dw(1, 1, 100, 256, 1, 0, 1, None) == 1001  # rows % 64
     assert lib.siren_inner_bwd_dw(1, 1, 128, 256, 1, 64, 1, None) == 1003  # bad tile
     assert lib.siren_dw_reduce(1, 1, 256, 0, 1, 1, None, None) == 1003     # tile must be explicit
@@ -89,15 +89,17 @@ def test_supported_hidden_sizes_validate(lib, hidden):
 
 def test_set_option_ranges(lib):
     """siren_set_option validates every knob on the host (SIREN_OPT_* in siren_hip.h) and leaves
-    the defaults restored; SIREN_OPT_NT_QUEUE takes 0 (static walk), 1 (forward modes), 2 (all)."""
+    the defaults restored; SIREN_OPT_NT_QUEUE takes 0 (static walk), 1 (forward modes), 2 (all).
+    The product library carries no measurement ablation: SIREN_OPT_NT_DIAG accepts only 0, and
+    the retired stagger (5) and prefetch-distance (7) options are rejected."""
     bad = 1003  # SIREN_ERR_CONFIG
-    for opt, good, wrong in ((0, (0, 128, 256), (64,)), (1, (0, 128, 256), (512,)), (2, (-1, 0, 7), (8, -2)),
-                             (3, (-1, 4), (5,)), (4, (0, 16), (-1,)), (5, (0, 64), (65,)),
-                             (6, (0, 1, 4, 512, 1024), (2, 8)), (7, (1, 16), (0, 17)), (8, (0, 1, 2), (3, -1))):
+    for opt, good, wrong in ((0, (0, 128, 256), (64,)), (1, (0, 128, 256), (512,)), (2, (-1, 0, 1, 4), (2, 3, 5, 7, -2)),
+                             (3, (-1, 4), (5,)), (4, (0, 16), (-1,)), (5, (), (0, 1)),
+                             (6, (0,), (1, 4, 512, 1024, 2, 8)), (7, (), (1, 2)), (8, (0, 1, 2), (3, -1))):
         for v in good:
             assert lib.siren_set_option(opt, v) == 0, (opt, v)
         for v in wrong:
             assert lib.siren_set_option(opt, v) == bad, (opt, v)
     assert lib.siren_set_option(99, 0) == bad
-    for opt, v in ((0, 0), (1, 0), (2, -1), (3, -1), (4, 0), (5, 0), (6, 0), (7, 2), (8, 1)):
+    for opt, v in ((0, 0), (1, 0), (2, -1), (3, -1), (4, 0), (6, 0), (8, 1)):
         assert lib.siren_set_option(opt, v) == 0

@@ -19,6 +19,7 @@ import numpy as np
 import pytest
 import torch
 
+from inr_for_audio_amd._lib import new_tileq
 from oracle import siren_oracle as orc
 from errlog import check_grads, log
 
@@ -109,7 +110,8 @@ def test_inner_fwd_act(lib, dev, tile, act, R, H, amag, head):
     hp = torch.zeros(H // 128, R, device=dev)
     ok(lib.siren_inner_fwd_act(ptr(to_dev(X, dev, H16)), ptr(to_dev(W, dev, H16)), ptr(to_dev(b, dev)), act,
                                ctypes.c_float(30.0), ptr(to_dev(a, dev)), R, H, ptr(Y), ptr(C), ptr(E),
-                               ptr(to_dev(hw, dev)) if head else None, ptr(hp) if head else None, S()), lib)
+                               ptr(to_dev(hw, dev)) if head else None, ptr(hp) if head else None,
+                               ptr(new_tileq(dev)), S()), lib)
     z = X.astype(np.float64) @ W.astype(np.float64).T + b
     # fp32 accumulation of z: |dz| ~ 1e-6; through sin(a z) that is a*|dz|
     slack = 2e-6 * max(1.0, float(amag)) * 4

@@ -1,9 +1,12 @@
-"""Dynamic tile queue of the ping-pong NT GEMM (SIREN_OPT_NT_QUEUE, gemm_nt.hip tileq_*).
+"""Dynamic tile queue of the ping-pong NT GEMM (SIREN_OPT_NT_QUEUE; caller-owned counter sets,
+include/siren_hip.h SIREN_TILEQ_INTS).
 
 The queue only changes WHICH persistent block computes a tile, never how, so every output must be
-bit-identical to the static walk: forward (with the head partials), dX and dX into layer 0, over
-grids where the shards hold one or several blocks, several launches in a row (the queue re-zeroes
-itself) and a second stream (its own counter set).  One case is also checked against fp64.
+bit-identical to the static walk: forward (with the head partials) over grids where the shards
+hold one or several blocks, several launches in a row on one set, a second stream with its own
+set, and a set handed over full of garbage (the launcher zeroes it on the stream first).  The
+backward modes through the queue (option 2) are checked on the fused step, whose siren_batch
+carries the set.  One case is also checked against fp64.
 """
 import ctypes
 import math
@@ -47,23 +50,22 @@ def _inputs(dev, R, H, seed):
     return X, W, b, hw, dZ, Cp, t
 
 
-def _run_all(lib, dev, R, H, inp, stream):
+def _run_all(lib, dev, R, H, inp, stream, tq):
+    """Forward with and without the head partials; tq: tile-queue set (None: static walk)."""
     X, W, b, hw, dZ, Cp, t = inp
     s = stream.cuda_stream
-    Y = torch.full((R, H), float("nan"), dtype=H16, device=dev)
-    C = torch.full_like(Y, float("nan"))
-    hp = torch.full((H // 128, R), float("nan"), device=dev)
-    dZp = torch.full_like(Y, float("nan"))
-    dbp = torch.full((R // 128, H), float("nan"), device=dev)
-    p0 = torch.full((R // 128, 3, H), float("nan"), device=dev)
-    WT = W.t().contiguous()
-    stream.wait_stream(torch.cuda.current_stream())  # the fills above ran on the current stream
-    ok(lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), P(hw), P(hp), s), lib)
-    ok(lib.siren_inner_bwd_dx(P(dZ), P(WT), P(Cp), ctypes.c_float(30.0), R, H, None, P(dZp), P(dbp), s), lib)
-    ok(lib.siren_first_bwd_dx(P(dZ), P(WT), P(Cp), P(t), 2, ctypes.c_float(3000.0), R, H, None, P(p0), s), lib)
-    stream.synchronize()
-    # the 256-tile launches write R/256 partial rows; the rest stays NaN in both runs
-    return [Y, C, hp[:H // 256], dZp, dbp[:R // 256], p0[:R // 256]]
+    res = []
+    for head in (False, True):
+        Y = torch.full((R, H), float("nan"), dtype=H16, device=dev)
+        C = torch.full_like(Y, float("nan"))
+        hp = torch.full((H // 128, R), float("nan"), device=dev)
+        stream.wait_stream(torch.cuda.current_stream())  # the fills above ran on the current stream
+        ok(lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), P(hw) if head else 0,
+                               P(hp) if head else 0, P(tq), s), lib)
+        stream.synchronize()
+        # the 256-tile launches write H/256 partial rows; the rest stays NaN in both runs
+        res += [Y, C] + ([hp[:H // 256]] if head else [])
+    return res
 
 
 def _same(a, b):
@@ -76,19 +78,41 @@ def _same(a, b):
                                       # 20 tiles: shards of 2 and 3 tiles (uneven eighths)
                                       (2560, 512, 8), (2560, 512, 16)])
 def test_queue_bit_identical_to_static_walk(lib, dev, R, H, grid):
+    from inr_for_audio_amd._lib import new_tileq
     ok(lib.siren_set_option(0, 256), lib)
     ok(lib.siren_set_option(2, 4), lib)
     ok(lib.siren_set_option(4, grid), lib)
     inp = _inputs(dev, R, H, seed=R + H + grid)
     st = torch.cuda.current_stream()
-    ok(lib.siren_set_option(8, 0), lib)
-    ref = _run_all(lib, dev, R, H, inp, st)
-    ok(lib.siren_set_option(8, 2), lib)  # every mode
-    for _ in range(3):  # back to back: each launch's last block re-zeroes the queue
-        assert _same(_run_all(lib, dev, R, H, inp, st), ref)
+    ref = _run_all(lib, dev, R, H, inp, st, None)
+    tq = new_tileq(dev)
+    for _ in range(3):  # back to back on one set
+        assert _same(_run_all(lib, dev, R, H, inp, st, tq), ref)
     side = torch.cuda.Stream(device=dev)
-    assert _same(_run_all(lib, dev, R, H, inp, side), ref)
-    assert _same(_run_all(lib, dev, R, H, inp, st), ref)
+    assert _same(_run_all(lib, dev, R, H, inp, side, new_tileq(dev)), ref)
+    assert _same(_run_all(lib, dev, R, H, inp, st, tq), ref)
+
+
+@pytest.mark.parametrize("fill", [1, -1, 1 << 30, "random"])
+def test_queue_set_handed_over_dirty(lib, dev, fill):
+    """A counter set left non-zero (an aborted launch, a caller's garbage) must not change any
+    output: every queue launch zeroes its set on the stream first, and every pulled tile id is
+    range-checked, so no block can skip a tile or walk past its shard."""
+    from inr_for_audio_amd._lib import TILEQ_INTS
+    R, H, grid = 4096, 1024, 16
+    ok(lib.siren_set_option(0, 256), lib)
+    ok(lib.siren_set_option(2, 4), lib)
+    ok(lib.siren_set_option(4, grid), lib)
+    inp = _inputs(dev, R, H, seed=5)
+    st = torch.cuda.current_stream()
+    ref = _run_all(lib, dev, R, H, inp, st, None)
+    if fill == "random":
+        g = torch.Generator(device=dev).manual_seed(1)
+        tq = torch.randint(-(1 << 31), (1 << 31) - 1, (TILEQ_INTS,), dtype=torch.int64, device=dev,
+                           generator=g).to(torch.int32)
+    else:
+        tq = torch.full((TILEQ_INTS,), fill, dtype=torch.int32, device=dev)
+    assert _same(_run_all(lib, dev, R, H, inp, st, tq), ref)
 
 
 @pytest.mark.parametrize("act", ["snake", "tanh"])
@@ -101,11 +125,12 @@ def test_queue_act_forward_bit_identical(lib, dev, act, grid):
     ok(lib.siren_set_option(0, 256), lib)
     ok(lib.siren_set_option(2, 4), lib)
     ok(lib.siren_set_option(4, grid), lib)
+    from inr_for_audio_amd._lib import new_tileq
     X, W, b, hw, *_ = _inputs(dev, R, H, seed=11)
     a = 0.5 + torch.rand(H, device=dev)
     s = torch.cuda.current_stream().cuda_stream
 
-    def run():
+    def run(tq):
         res = []
         for head in (False, True):
             Y = torch.full((R, H), float("nan"), dtype=H16, device=dev)
@@ -114,14 +139,12 @@ def test_queue_act_forward_bit_identical(lib, dev, act, grid):
             hp = torch.full((H // 128, R), float("nan"), device=dev)
             ok(lib.siren_inner_fwd_act(P(X), P(W), P(b), code, ctypes.c_float(1.0), P(a), R, H, P(Y), P(C),
                                        P(E) if act == "snake" else 0, P(hw) if head else 0, P(hp) if head else 0,
-                                       s), lib)
+                                       P(tq), s), lib)
             torch.cuda.synchronize()
             res += [Y, C] + ([E] if act == "snake" else []) + ([hp[:H // 256]] if head else [])
         return res
-    ok(lib.siren_set_option(8, 0), lib)
-    ref = run()
-    ok(lib.siren_set_option(8, 1), lib)
-    assert _same(run(), ref)
+    ref = run(None)
+    assert _same(run(new_tileq(dev)), ref)
 
 
 def test_queue_forward_vs_fp64(lib, dev):
@@ -129,11 +152,59 @@ def test_queue_forward_vs_fp64(lib, dev):
     ok(lib.siren_set_option(0, 256), lib)
     ok(lib.siren_set_option(2, 4), lib)
     ok(lib.siren_set_option(4, 16), lib)
+    from inr_for_audio_amd._lib import new_tileq
     X, W, b, hw, *_ = _inputs(dev, R, H, seed=3)
-    Y, C, hp = _run_all(lib, dev, R, H, _inputs(dev, R, H, seed=3), torch.cuda.current_stream())[:3]
+    Y, C, hp = _run_all(lib, dev, R, H, _inputs(dev, R, H, seed=3), torch.cuda.current_stream(), new_tileq(dev))[2:]
     a = 30.0 * (X.double() @ W.double().t() + b.double())
     for got, ref in ((Y, torch.sin(a)), (C, torch.cos(a))):
         err = (got.double() - ref).abs() - ref.abs() * 2.0 ** -11 - 2e-5
         assert float(err.max()) <= 0
     head = hp.double().sum(0)
     assert float((head - torch.sin(a) @ hw.double()).abs().max()) < 1e-4
+
+
+def _engine(dev, seed, H=512, n=65536):
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(seed)
+    model = SirenWithSnakeTanh(1, 1, H, 2, 0, 0, first_omega_0=2000.0, hidden_omega_0=30.0)
+    t = torch.linspace(-1, 1, n).reshape(n, 1)
+    y = torch.sin(37 * t + seed) * 0.5
+    return SirenEngine(model, t, y, device=dev)
+
+
+def test_queue_every_mode_in_the_fused_step(lib, dev):
+    """SIREN_OPT_NT_QUEUE 2 sends the dX / dX0 launches of siren_train_step through the batch's
+    set too: the step's gradients are bit-identical to the static walk's (0) and the default (1)."""
+    assert lib.siren_nt_tile(65536, 512) == 256
+    grads = []
+    for q in (0, 1, 2):
+        ok(lib.siren_set_option(8, q), lib)
+        e = _engine(dev, 0)
+        e.step()
+        torch.cuda.synchronize()
+        grads.append(e.grads.clone())
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
+
+
+def test_two_captured_graphs_replayed_concurrently(lib, dev):
+    """Two engines, each step captured as a HIP graph (each workspace owns its counter set), are
+    replayed at the same time on two streams: both stay bit-identical to their eager twins.  (The
+    round-2 design keyed one global set per capture stream, which two replays could share.)"""
+    eager = [_engine(dev, s) for s in (1, 2)]
+    graphed = [_engine(dev, s) for s in (1, 2)]
+    for e in eager:
+        for _ in range(4):
+            e.step()
+    for e in graphed:
+        e.step()
+        e.capture_graph()
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for e, st in zip(graphed, streams):
+            with torch.cuda.stream(st):
+                e.graph.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(eager, graphed):
+        assert torch.equal(a.params, b.params)

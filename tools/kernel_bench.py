@@ -26,14 +26,12 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tiles", default="128,256")
-    ap.add_argument("--pipes", default="1,4", help="256x256 NT K-loop variants to time (0..4)")
+    ap.add_argument("--pipes", default="1,4", help="256x256 NT K-loop variants to time (0, 1, 4)")
     ap.add_argument("--tn-pipes", default="0,3", help="256x256 dW K-loop variants to time (0..3)")
     ap.add_argument("--only", default="", help="comma list of case-name prefixes to run")
-    ap.add_argument("--staggers", default="", help="SIREN_OPT_NT_STAGGER values to add as "
-                    "extra persistent NT cases")
     ap.add_argument("--diags", default="", help="SIREN_OPT_NT_DIAG ablation bits to add as extra "
-                    "NT cases (1: L2-resident X; pipe 4: 512 no tiles, 1024 no epilogue); timing only")
-    ap.add_argument("--pf-dists", default="2", help="SIREN_OPT_NT_PF_DIST values for NT pipe 5")
+                    "NT cases (1: L2-resident X; pipe 4: 512 no tiles, 1024 no epilogue); timing only, "
+                    "needs --lib of a SIREN_DIAG build")
     ap.add_argument("--dw-splits", default="", help="extra dW cases at these split-K counts (256 tile)")
     ap.add_argument("--grids", default="", help="SIREN_OPT_NT_GRID persistent grid sizes to add as extra "
                     "ping-pong NT cases (measurement: CU-count scaling)")
@@ -45,7 +43,9 @@ def main():
     import __graft_entry__ as ge
     ge.build()
     from inr_for_audio_amd import _lib
-    lib = _lib.load(os.path.join(ROOT, args.lib)) if args.lib else _lib.load()
+    # a fresh handle: _lib.load() has already cached the product library (ge.build() loads it), so
+    # until round 3 `--lib` silently timed the product library against itself
+    lib = _lib.bind(os.path.join(ROOT, args.lib)) if args.lib else _lib.load()
     dev = torch.device("cuda:0")
     R, H = args.rows, args.hidden
     s = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
@@ -70,11 +70,14 @@ def main():
     tiles = [int(x) for x in args.tiles.split(",")]
     flops = 2.0 * R * H * H
 
+    tq = _lib.new_tileq(dev)
+
     def run_fwd():
-        return lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), None, None, s())
+        return lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), None, None, P(tq), s())
 
     def run_fwd_head():
-        return lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), P(hw), P(hp), s())
+        return lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), P(hw), P(hp), P(tq),
+                                   s())
 
     def run_dx():
         return lib.siren_inner_bwd_dx(P(dZ), P(WT), P(C), ctypes.c_float(30.0), R, H, None, P(dZp), P(part),
@@ -97,15 +100,12 @@ def main():
         return lib.siren_inner_bwd_dw(P(Y), P(dZ), R, H, splits, tile, P(slabs[splits]), s())
 
     cases = {}
-    pfd = {}
     pipes = [int(x) for x in args.pipes.split(",")]
     for tile in tiles:
         for pipe in (pipes if tile == 256 else [0]):
-            for d in ([int(x) for x in args.pf_dists.split(",")] if pipe == 5 else [0]):
-                sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "") + (f"f{d}" if d else "")
-                for nm, fn in (("fwd", run_fwd), ("fwd_head", run_fwd_head), ("dx", run_dx), ("dx0", run_dx0)):
-                    cases[f"{nm}_{sfx}"] = (tile, pipe, fn, flops)
-                    pfd[f"{nm}_{sfx}"] = d
+            sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "")
+            for nm, fn in (("fwd", run_fwd), ("fwd_head", run_fwd_head), ("dx", run_dx), ("dx0", run_dx0)):
+                cases[f"{nm}_{sfx}"] = (tile, pipe, fn, flops)
         for pipe in ([int(x) for x in args.tn_pipes.split(",")] if tile == 256 else [0]):
             sfx = f"t{tile}" + (f"p{pipe}" if tile == 256 else "")
             cases[f"dw_{sfx}"] = (tile, pipe, (lambda tl=tile: run_dw(tl)), flops)
@@ -134,19 +134,12 @@ def main():
     if args.only:
         pre = tuple(args.only.split(","))
         cases = {k: v for k, v in cases.items() if k.startswith(pre)}
-    stagger = {k: 0 for k in cases}
-    for v in [int(x) for x in args.staggers.split(",") if x]:
-        for k, c in list(cases.items()):
-            if v and (k.endswith("p1") or k.endswith("p4")) and not k.startswith("dw") and stagger[k] == 0:
-                cases[f"{k}_s{v}"] = c
-                stagger[f"{k}_s{v}"] = v
     diag = {k: 0 for k in cases}
     for v in [int(x) for x in args.diags.split(",") if x]:
         for k, c in list(cases.items()):
-            if k.startswith(("fwd", "dx")) and stagger.get(k, 0) == 0 and diag[k] == 0:
+            if k.startswith(("fwd", "dx")) and diag[k] == 0:
                 cases[f"{k}_d{v}"] = c
                 diag[f"{k}_d{v}"] = v
-                stagger[f"{k}_d{v}"] = 0
     queue = {k: 1 for k in cases}
     if args.queue_ab:
         for k, c in list(cases.items()):
@@ -154,15 +147,13 @@ def main():
                 for q in (0, 2):
                     cases[f"{k}_q{q}"] = c
                     queue[f"{k}_q{q}"] = q
-                    stagger[f"{k}_q{q}"] = stagger.get(k, 0)
     grid = {k: 0 for k in cases}
     for v in [int(x) for x in args.grids.split(",") if x]:
         for k, c in list(cases.items()):
             if k.startswith(("fwd", "dx")) and "p4" in k and diag.get(k, 0) == 0 and queue.get(k, 1) == 1 \
-                    and grid.get(k, 0) == 0 and stagger.get(k, 0) == 0:
+                    and grid.get(k, 0) == 0:
                 cases[f"{k}_g{v}"] = c
                 grid[f"{k}_g{v}"] = v
-                stagger[f"{k}_g{v}"] = 0
     times = {k: [] for k in cases}
     for _ in range(args.rounds):
         for name, (tile, pipe, fn, _) in cases.items():
@@ -176,12 +167,9 @@ def main():
                 torch.cuda.synchronize()
                 times[name].append(ev0.elapsed_time(ev1) / args.reps)
                 continue
-            _lib.check(lib.siren_set_option(5, stagger[name]), "stagger option")
             _lib.check(lib.siren_set_option(6, diag.get(name, 0)), "diag option")
             _lib.check(lib.siren_set_option(8, queue.get(name, 1)), "queue option")
             _lib.check(lib.siren_set_option(4, grid.get(name, 0)), "grid option")
-            if pfd.get(name, 0):
-                lib.siren_set_option(7, pfd[name])
             lib.siren_set_option(0, tile if not name.startswith("dw") else 0)
             if name.startswith("dw"):
                 lib.siren_set_option(3, pipe)
@@ -196,7 +184,6 @@ def main():
             ev1.record()
             torch.cuda.synchronize()
             times[name].append(ev0.elapsed_time(ev1) / args.reps)
-    lib.siren_set_option(5, 0)
     lib.siren_set_option(6, 0)
     lib.siren_set_option(8, 1)
     lib.siren_set_option(4, 0)

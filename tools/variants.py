@@ -1,0 +1,100 @@
+"""Measurement-only variants of the product kernels, kept OUT of the product source: each variant is
+a set of textual patches applied to a temporary copy of inr-for-audio_amd/csrc, compiled to
+inr-for-audio_amd/libsiren_<name>.so (never loaded by the package; tools/ab_bench.py times it
+beside the product library in one process and checks bit-identity).
+
+    python tools/variants.py st_nt fl        # build
+    python tools/ab_bench.py --libs base=inr-for-audio_amd/libsiren_hip.so,fl=inr-for-audio_amd/libsiren_fl.so
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "inr-for-audio_amd", "csrc")
+SOURCES = ["capi.hip", "gemm_nt.hip", "gemm_tn.hip", "elementwise.hip", "kan.hip", "layer_fp32.hip"]
+
+_ST16 = "  auto st16 = [&](h16* dst, uint4 v) { *(uint4*)dst = v; };"
+
+
+def _st16_asm(pol: str) -> str:
+    # the asm store carries its own s_nop: a VALU write of the data VGPRs must wait a cycle after a
+    # 128-bit store, which hipcc's hazard recognizer does not see inside inline asm
+    return ("  auto st16 = [&](h16* dst, uint4 v) {\n"
+            "    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));\n"
+            "    const u32x4 w = u32x4{v.x, v.y, v.z, v.w};\n"
+            f"    asm volatile(\"global_store_dwordx4 %0, %1, off {pol}\\n\\ts_nop 1\" ::\"v\"(dst), \"v\"(w) : \"memory\");\n"
+            "  };")
+
+
+_FL_OLD = """#pragma unroll
+        for (int pp = 0; pp < SN / 2; ++pp) {
+          st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
+          st16(p.C + rowoff + npc + pp * 32, cpk[pp]);
+          if constexpr (MODE == NT_FWD_SNAKE) st16(p.E + rowoff + npc + pp * 32, epk[pp]);
+        }"""
+# whole 128-B lines: lanes l and l^8 (rows r, r^8 of the subtile) trade one 16-B piece by DPP
+# row_ror:8, so each store instruction writes 8 whole row segments instead of 16 half ones
+_FL_NEW = """if constexpr (SN == 4 && MODE == NT_FWD) {
+          const bool hi = (lane & 8) != 0;
+          const size_t ra = (size_t)(m0 + wm * TM + j * 16 + (lane & 7)) * N + npc + (hi ? 32 : 0);
+          auto fl_store = [&](h16* dst, const uint4 (&pc)[SN / 2]) {
+            const uint4 send = hi ? pc[0] : pc[1];
+            uint4 recv;
+            recv.x = __builtin_amdgcn_update_dpp(0, (int)send.x, 0x128, 0xf, 0xf, false);
+            recv.y = __builtin_amdgcn_update_dpp(0, (int)send.y, 0x128, 0xf, 0xf, false);
+            recv.z = __builtin_amdgcn_update_dpp(0, (int)send.z, 0x128, 0xf, 0xf, false);
+            recv.w = __builtin_amdgcn_update_dpp(0, (int)send.w, 0x128, 0xf, 0xf, false);
+            st16(dst + ra, hi ? recv : pc[0]);
+            st16(dst + ra + (size_t)8 * N, hi ? pc[1] : recv);
+          };
+          fl_store(p.Y, yp);
+          fl_store(p.C, cpk);
+        } else {
+#pragma unroll
+          for (int pp = 0; pp < SN / 2; ++pp) {
+            st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
+            st16(p.C + rowoff + npc + pp * 32, cpk[pp]);
+            if constexpr (MODE == NT_FWD_SNAKE) st16(p.E + rowoff + npc + pp * 32, epk[pp]);
+          }
+        }"""
+
+VARIANTS = {
+    "st_sc1": {"gemm_nt.hip": [(_ST16, _st16_asm("sc1"))]},          # write-through epilogue stores
+    "st_nt": {"gemm_nt.hip": [(_ST16, _st16_asm("nt"))]},            # non-temporal epilogue stores
+    "st_sc0sc1": {"gemm_nt.hip": [(_ST16, _st16_asm("sc0 sc1"))]},
+    "fl": {"gemm_nt.hip": [(_FL_OLD, _FL_NEW)]},                     # whole-line forward stores
+}
+
+
+def build(name: str, extra_defines=()) -> str:
+    patches = VARIANTS[name]
+    out = os.path.join(ROOT, "inr-for-audio_amd", f"libsiren_{name}.so")
+    with tempfile.TemporaryDirectory() as tmp:
+        for f in os.listdir(CSRC):
+            shutil.copy(os.path.join(CSRC, f), tmp)
+        for f, reps in patches.items():
+            p = os.path.join(tmp, f)
+            s = open(p).read()
+            for old, new in reps:
+                if old not in s:
+                    raise SystemExit(f"variant {name}: patch target not found in {f}")
+                s = s.replace(old, new)
+            open(p, "w").write(s)
+        capi = os.path.join(tmp, "capi.hip")
+        s = open(capi).read().replace('"../../include/siren_hip.h"', f'"{ROOT}/include/siren_hip.h"')
+        open(capi, "w").write(s)
+        cmd = [os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), "--offload-arch=gfx950", "-O3", "-std=c++17",
+               "-fPIC", "-shared", "-ffp-contract=off", *[f"-D{d}" for d in extra_defines],
+               *[os.path.join(tmp, f) for f in SOURCES], "-o", out]
+        subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
+    return out
+
+
+if __name__ == "__main__":
+    for nm in sys.argv[1:]:
+        print(build(nm))
