@@ -294,7 +294,8 @@ int siren_fp32_linear_bwd(const float* x, int64_t rows, int32_t in, int32_t out,
  * Layer l maps width[l] -> width[l+1] as efficient-KAN's KANLinear (kan.py:6-166) with
  * grid_size 5, spline_order 3, SiLU base: out = SiLU(x) base_w^T + B(x) (spline_w*scaler)^T,
  * B = the 8 order-3 B-spline bases on the layer's `grid` buffer [in][12].  fp32 throughout.
- * The last width must be 1.  Workspace: one caller-owned fp32 buffer of
+ * siren_kan_forward / _backward take any last width (out is then [rows][last width]); the fused
+ * fit step (siren_kan_train_step) needs last width 1.  Workspace: one caller-owned fp32 buffer of
  * siren_kan_workspace_floats(net, rows, splits) floats (activations, combined weights,
  * gradients of the layer outputs, split-K slabs -- the expansions are never stored). */
 #define SIREN_KAN_MAX_LAYERS 8
@@ -327,9 +328,15 @@ typedef struct siren_kan_batch {
 int64_t siren_kan_workspace_floats(const siren_kan_net* net, int32_t rows, int32_t splits);
 /* run.py:255 model(model_input) for arch='kan' */
 int siren_kan_forward(const siren_kan_net* net, siren_kan_batch* batch, void* stream);
-/* run.py:158-185 for arch='kan': forward + MSELoss + backward; gradients ACCUMULATE */
+/* run.py:158-185 for arch='kan': forward + MSELoss + backward; gradients ACCUMULATE (last width 1) */
 int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* grads, siren_kan_batch* batch,
                          void* stream);
+/* autograd of siren_kan_forward (kan.py:153-166, 268-273) for an arbitrary upstream gradient:
+ * batch->g holds dLoss/dout [rows][last width] and batch->ws the workspace of a siren_kan_forward
+ * of the same coords, rows and splits; gradients ACCUMULATE (zero_grads + flat: memset first);
+ * grad_coords != NULL also receives dLoss/dcoords [rows][width[0]] (grads->sse is not used). */
+int siren_kan_backward(const siren_kan_net* net, const siren_kan_grads* grads, siren_kan_batch* batch,
+                       float* grad_coords, void* stream);
 
 /* ---- per-launch HIP-event profiling of the fused path (bench.py) --------------------
  * siren_profile_enable(n) creates 2n hipEvents; while enabled every launch made by

@@ -158,6 +158,8 @@ _SIGS = {
     "siren_kan_forward": (ctypes.c_int, [ctypes.POINTER(SirenKanNet), ctypes.POINTER(SirenKanBatch), _p]),
     "siren_kan_train_step": (ctypes.c_int, [ctypes.POINTER(SirenKanNet), ctypes.POINTER(SirenKanGrads),
                                             ctypes.POINTER(SirenKanBatch), _p]),
+    "siren_kan_backward": (ctypes.c_int, [ctypes.POINTER(SirenKanNet), ctypes.POINTER(SirenKanGrads),
+                                          ctypes.POINTER(SirenKanBatch), _p, _p]),
     "siren_profile_enable": (ctypes.c_int, [_i32]),
     "siren_profile_reset": (ctypes.c_int, []),
     "siren_profile_mask": (ctypes.c_int, [ctypes.c_uint32]),

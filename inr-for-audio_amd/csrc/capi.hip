@@ -647,7 +647,6 @@ int check_kan(const siren_kan_net* n) {
   if (n->n_layers < 1 || n->n_layers > SIREN_KAN_MAX_LAYERS) return SIREN_ERR_CONFIG;
   for (int l = 0; l <= n->n_layers; ++l)
     if (n->width[l] < 1 || n->width[l] > 4096) return SIREN_ERR_SHAPE;
-  if (n->width[n->n_layers] != 1) return SIREN_ERR_SHAPE;
   for (int l = 0; l < n->n_layers; ++l)
     if (!n->grid[l] || !n->base_w[l] || !n->spline_w[l] || !n->scaler[l]) return SIREN_ERR_NULL;
   return SIREN_OK;
@@ -722,6 +721,40 @@ hipError_t kan_run_forward(const siren_kan_net* n, const siren_kan_batch* b, con
   return hipSuccess;
 }
 
+// backward of layers l_top .. 0 from G = dLoss/dX[l_top + 1] ([R][out]); the layer inputs X[l] and
+// the combined weights are the workspace's from the forward.  grad_coords != NULL: also dLoss/dcoords
+// ([R][width[0]]), the first layer's input gradient (the fit itself never needs it).
+hipError_t kan_run_backward(const siren_kan_net* net, const siren_kan_grads* gr, const siren_kan_batch* b,
+                            const KanWs& w, hipStream_t s, const float* G, int l_top, int cur, float* grad_coords) {
+  const int64_t R = b->rows;
+  for (int l = l_top; l >= 0; --l) {
+    const int in = net->width[l], out = net->width[l + 1];
+    const float* xl = l == 0 ? b->coords : w.X[l];
+    const int64_t max_splits = w.slab_floats / ((int64_t)out * KAN_K1 * in);
+    float* gin = l > 0 ? w.G[cur] : grad_coords;
+    if (out <= 64 && gin) {
+      // dW and dX = SiLU' dA_base + sum_c B'_c dA_c in one pass (bases and G read once)
+      SIREN_PROF(SIREN_PROF_KAN_DX, s, kan_bwd_fused(xl, net->grid[l], G, w.WT[l], R, in, out, max_splits, w.slab,
+                                                     w.dW, gin, s));
+      SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
+                                                         gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
+      G = gin;
+      cur ^= 1;
+      continue;
+    }
+    // dW[o][k] = sum_r G[r][o] A[r][k]  (split-K over the coordinates, bases recomputed)
+    SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_dw_fused(xl, net->grid[l], G, R, in, out, max_splits, w.slab, w.dW, s));
+    SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
+                                                       gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
+    if (!gin) break;  // layer 0 without a coordinate gradient
+    // dX = SiLU' dA_base + sum_c B'_c dA_spline_c with dA = G W formed per chunk in LDS
+    SIREN_PROF(SIREN_PROF_KAN_DX, s, kan_dx_fused(xl, net->grid[l], G, w.WT[l], R, in, out, gin, s));
+    G = gin;
+    cur ^= 1;
+  }
+  return hipSuccess;
+}
+
 }  // namespace
 
 extern "C" {
@@ -741,6 +774,10 @@ int siren_kan_forward(const siren_kan_net* net, siren_kan_batch* b, void* stream
   const KanWs w = kan_layout(net, b->rows, b->splits, b->ws);
   SIREN_TRY(hipMemsetAsync(w.zero, 0, sizeof(float), s));
   SIREN_TRY(kan_run_forward(net, b, w, s, net->n_layers));
+  const int wl = net->width[net->n_layers];
+  if (wl != 1)  // a lone KANLinear / a KAN with a wide last layer: out = X[L] as it stands
+    return (int)hipMemcpyAsync(b->out, w.X[net->n_layers], (size_t)b->rows * wl * sizeof(float),
+                               hipMemcpyDeviceToDevice, s);
   SIREN_TRY(head_loss(w.X[net->n_layers], 1, b->rows, w.zero, b->out, 0, 0.f, b->out, b->g, w.sse_part,
                       w.gsum_part, nullptr, s));
   return SIREN_OK;
@@ -755,6 +792,7 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, si
     return SIREN_ERR_SHAPE;
   for (int l = 0; l < net->n_layers; ++l)
     if (!gr->base_w[l] || !gr->spline_w[l] || !gr->scaler[l]) return SIREN_ERR_NULL;
+  if (net->width[net->n_layers] != 1) return SIREN_ERR_SHAPE;  // MSELoss on a scalar output
   hipStream_t s = S(stream);
   const int64_t R = b->rows;
   const KanWs w = kan_layout(net, R, b->splits, b->ws);
@@ -790,31 +828,23 @@ int siren_kan_train_step(const siren_kan_net* net, const siren_kan_grads* gr, si
     SIREN_PROF(SIREN_PROF_KAN_MISC, s, sum_to(w.sse_part, (int)((R + 255) / 256), gr->sse, 1, s));
   }
   // backward (autograd of run.py:185): G = dLoss/dX[l+1], [R][out]
-  for (int l = l_top; l >= 0; --l) {
-    const int in = net->width[l], out = net->width[l + 1];
-    const float* xl = l == 0 ? b->coords : w.X[l];
-    const int64_t max_splits = w.slab_floats / ((int64_t)out * KAN_K1 * in);
-    if (l > 0 && out <= 64) {
-      // dW and dX = SiLU' dA_base + sum_c B'_c dA_c in one pass (bases and G read once)
-      SIREN_PROF(SIREN_PROF_KAN_DX, s, kan_bwd_fused(xl, net->grid[l], G, w.WT[l], R, in, out, max_splits, w.slab,
-                                                     w.dW, w.G[cur], s));
-      SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
-                                                         gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
-      G = w.G[cur];
-      cur ^= 1;
-      continue;
-    }
-    // dW[o][k] = sum_r G[r][o] A[r][k]  (split-K over the coordinates, bases recomputed)
-    SIREN_PROF(SIREN_PROF_KAN_DW, s, kan_dw_fused(xl, net->grid[l], G, R, in, out,
-                                                    w.slab_floats / ((int64_t)out * KAN_K1 * in), w.slab, w.dW, s));
-    SIREN_PROF(SIREN_PROF_KAN_MISC, s, kan_param_grads(w.dW, net->spline_w[l], net->scaler[l], out, in, 1,
-                                                       gr->base_w[l], gr->spline_w[l], gr->scaler[l], s));
-    if (l == 0) break;
-    // dX = SiLU' dA_base + sum_c B'_c dA_spline_c with dA = G W formed per chunk in LDS
-    SIREN_PROF(SIREN_PROF_KAN_DX, s, kan_dx_fused(xl, net->grid[l], G, w.WT[l], R, in, out, w.G[cur], s));
-    G = w.G[cur];
-    cur ^= 1;
-  }
+  SIREN_TRY(kan_run_backward(net, gr, b, w, s, G, l_top, cur, nullptr));
+  return SIREN_OK;
+}
+
+int siren_kan_backward(const siren_kan_net* net, const siren_kan_grads* gr, siren_kan_batch* b,
+                       float* grad_coords, void* stream) {
+  int st = check_kan(net);
+  if (st) return st;
+  if (!b || !gr) return SIREN_ERR_NULL;
+  if (!b->coords || !b->g || !b->ws) return SIREN_ERR_NULL;
+  if (b->rows < 1 || b->splits < 1) return SIREN_ERR_SHAPE;
+  for (int l = 0; l < net->n_layers; ++l)
+    if (!gr->base_w[l] || !gr->spline_w[l] || !gr->scaler[l]) return SIREN_ERR_NULL;
+  hipStream_t s = S(stream);
+  const KanWs w = kan_layout(net, b->rows, b->splits, b->ws);
+  if (b->zero_grads && gr->flat) SIREN_TRY(hipMemsetAsync(gr->flat, 0, gr->flat_len * sizeof(float), s));
+  SIREN_TRY(kan_run_backward(net, gr, b, w, s, b->g, net->n_layers - 1, 0, grad_coords));
   return SIREN_OK;
 }
 

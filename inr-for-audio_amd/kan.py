@@ -9,9 +9,12 @@ scaler), so ``torch.manual_seed(s)`` gives bit-identical parameters.  The B-spli
 for that fit is the Cox-de Boor recursion of kan.py:94-104, vectorised over knots.
 
 Supported like run.py uses it: grid_size 5, spline_order 3, SiLU base activation,
-standalone spline scaler, last width 1.  ``forward`` is HIP inference (no autograd: fitting
-goes through ``KanEngine`` / ``run.train(arch='kan')``); grid updates and the regularisation
-loss (not used by run.py) are not on the path.
+standalone spline scaler.  ``KAN.forward`` and ``KANLinear.forward`` are differentiable
+(``_KanFunction``: siren_kan_forward, then siren_kan_backward for any upstream gradient, into the
+parameters and, when asked for, the input), so a user loop with ``loss.backward()`` and
+``torch.optim`` trains them as it trains the reference's modules (kan.py:153-166, 268-273); the
+fused fit goes through ``KanEngine`` / ``run.train(arch='kan')``.  Grid updates and the
+regularisation loss (not used by run.py) are not on the path.
 """
 from __future__ import annotations
 
@@ -85,8 +88,80 @@ class KANLinear(torch.nn.Module):
         s = self.spline_scaler.unsqueeze(-1) if self.enable_standalone_scale_spline else 1.0
         return self.spline_weight * s
 
-    def forward(self, x):
-        raise NotImplementedError("a lone KANLinear has no HIP entry point: call the KAN")
+    def forward(self, x: torch.Tensor):
+        """kan.py:153-166: (..., in) -> (..., out), a one-layer KAN on the HIP path (differentiable)."""
+        _hip_check_layer(self)
+        return _kan_apply([self.in_features, self.out_features], [self], x,
+                          [self.base_weight, self.spline_weight, self.spline_scaler])
+
+
+def _hip_check_layer(lay: "KANLinear"):
+    if lay.grid_size != 5 or lay.spline_order != 3:
+        raise NotImplementedError("HIP KAN path: grid_size=5, spline_order=3 (kan.py defaults)")
+    if not lay.enable_standalone_scale_spline or not isinstance(lay.base_activation, torch.nn.SiLU):
+        raise NotImplementedError("HIP KAN path: SiLU base and a standalone spline scaler")
+
+
+def _kan_splits(rows: int) -> int:
+    return max(1, min(256, rows // 2048))
+
+
+def _net(widths, layers, params) -> SirenKanNet:
+    n = SirenKanNet()
+    n.n_layers = len(layers)
+    for l, w in enumerate(widths):
+        n.width[l] = w
+    for l, lay in enumerate(layers):
+        n.grid[l] = ptr(lay.grid)
+        n.base_w[l], n.spline_w[l], n.scaler[l] = (ptr(t) for t in params[3 * l:3 * l + 3])
+    return n
+
+
+class _KanFunction(torch.autograd.Function):
+    """HIP forward (siren_kan_forward) and backward (siren_kan_backward, any upstream gradient) of
+    a KANLinear stack; params = (base_weight, spline_weight, spline_scaler) per layer."""
+
+    @staticmethod
+    def forward(ctx, widths, layers, x, *params):
+        lib = _lib.load()
+        if not x.is_cuda:
+            raise RuntimeError("KAN runs on the HIP path only (CUDA tensors)")
+        dev = x.device
+        p = [t.detach().contiguous().float() for t in params]
+        net = _net(widths, layers, p)
+        xs = x.detach().reshape(-1, widths[0]).contiguous().float()
+        rows = xs.shape[0]
+        splits = _kan_splits(rows)
+        ws = torch.empty(int(lib.siren_kan_workspace_floats(ctypes.byref(net), rows, splits)), device=dev)
+        out = torch.empty(rows, widths[-1], dtype=torch.float32, device=dev)
+        g = torch.zeros(rows, widths[-1], dtype=torch.float32, device=dev)
+        b = SirenKanBatch()
+        b.rows, b.n_valid, b.n_total, b.splits, b.zero_grads = rows, 0, 1.0, splits, 0
+        b.coords, b.target, b.out, b.g, b.ws = ptr(xs), 0, ptr(out), ptr(g), ptr(ws)
+        check(lib.siren_kan_forward(ctypes.byref(net), ctypes.byref(b), torch.cuda.current_stream(dev).cuda_stream),
+              "siren_kan_forward")
+        ctx.keep = (net, b, ws, xs, g, p, x.shape, [t.shape for t in params])
+        return out.reshape(*x.shape[:-1], widths[-1])
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        lib = _lib.load()
+        net, b, ws, xs, g, p, xshape, shapes = ctx.keep
+        dev = xs.device
+        g.copy_(grad_out.reshape(g.shape).float())
+        grads = [torch.zeros(shp, dtype=torch.float32, device=dev) for shp in shapes]
+        gs = SirenKanGrads()
+        for l in range(len(shapes) // 3):
+            gs.base_w[l], gs.spline_w[l], gs.scaler[l] = (ptr(t) for t in grads[3 * l:3 * l + 3])
+        gx = torch.empty_like(xs) if ctx.needs_input_grad[2] else None
+        check(lib.siren_kan_backward(ctypes.byref(net), ctypes.byref(gs), ctypes.byref(b), ptr(gx),
+                                     torch.cuda.current_stream(dev).cuda_stream), "siren_kan_backward")
+        ctx.keep = None
+        return (None, None, None if gx is None else gx.reshape(xshape), *grads)
+
+
+def _kan_apply(widths, layers, x, params):
+    return _KanFunction.apply(list(widths), list(layers), x, *params)
 
 
 class KAN(torch.nn.Module):
@@ -109,8 +184,7 @@ class KAN(torch.nn.Module):
         if len(self.layers) > _lib.KAN_MAX_LAYERS or self.widths[-1] != 1:
             raise NotImplementedError(f"HIP KAN path: <= {_lib.KAN_MAX_LAYERS} layers, last width 1")
         for lay in self.layers:
-            if not lay.enable_standalone_scale_spline or not isinstance(lay.base_activation, torch.nn.SiLU):
-                raise NotImplementedError("HIP KAN path: SiLU base and a standalone spline scaler")
+            _hip_check_layer(lay)
 
     def param_index(self):
         pos = {n: k for k, (n, _) in enumerate(self.named_parameters())}
@@ -131,17 +205,20 @@ class KAN(torch.nn.Module):
             n.base_w[l], n.spline_w[l], n.scaler[l] = ptr(params[ib]), ptr(params[isp]), ptr(params[isc])
         return n
 
-    @torch.no_grad()
     def forward(self, x: torch.Tensor, update_grid=False):
-        """(..., in) CUDA coords -> (..., 1) through siren_kan_forward (inference)."""
+        """kan.py:268-273: (..., in) CUDA coords -> (..., out).  Differentiable when autograd needs
+        it (siren_kan_forward + siren_kan_backward); chunked HIP inference otherwise."""
         if update_grid:
             raise NotImplementedError("update_grid is not on the HIP path (run.py never uses it)")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("KAN.forward is HIP inference; fit with KanEngine / train(arch='kan')")
         if not x.is_cuda:
             raise RuntimeError("KAN.forward runs on the HIP path only (CUDA tensors)")
+        self.hip_check()
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            params = [t for lay in self.layers for t in (lay.base_weight, lay.spline_weight, lay.spline_scaler)]
+            return _kan_apply(self.widths, self.layers, x, params)
         lead = x.shape[:-1]
-        out = kan_forward(self, x.reshape(-1, self.widths[0]), x.device)
+        with torch.no_grad():
+            out = kan_forward(self, x.reshape(-1, self.widths[0]), x.device)
         return out.reshape(*lead, 1)
 
 

@@ -320,21 +320,23 @@ def checkpoint_fixture(ref_models, ref_utils):
 
 
 def fullsize_seed_trajectories(ref_models, ref_utils, seeds, steps, patience, omega0=3000.0, lr=1e-3,
-                               fname="trajectory_5x1024_w3000_seeds.json"):
+                               fname="trajectory_5x1024_w3000_seeds.json", duration=1):
     """The headline model (SIREN 5x1024, BASELINE cfg2's shape) fitted full batch on gt_bach
-    1 s over several init seeds -- the 0.1 dB fit-parity fixture at the model size the
-    north_star quotes.  The plateau patience is lowered (run.py:117 uses 200) so that the
-    CPU-affordable step count still contains ReduceLROnPlateau drops; the GPU test uses the
-    same patience.  Written after every seed (the run takes ~1 h on 8 CPU threads)."""
+    (`duration` s: 1, or 6 = 264 600 coordinates, the longest whole-second clip gt_bach holds
+    and the closest to cfg2's 10 s) over several init seeds -- the 0.1 dB fit-parity fixture at
+    the model size the north_star quotes.  The plateau patience can be lowered (run.py:117 uses
+    200) so that the CPU-affordable step count contains ReduceLROnPlateau drops; the GPU test
+    uses the same patience.  Written after every seed (6 s: ~13 s per step on 8 CPU threads)."""
     wav = os.path.join(REF, "gt_bach.wav")
-    coords, target = ref_utils.WaveformFitting(wav, duration=1, decimation=1)[0]
+    coords, target = ref_utils.WaveformFitting(wav, duration=duration, decimation=1)[0]
     tgt = target.numpy().reshape(-1)
     path = os.path.join(OUT, fname)
     out = {"steps": steps, "omega0": omega0, "hidden": 1024, "num_sine": 4, "patience": patience,
-           "factor": 0.8, "lr0": lr, "runs": {}}
+           "factor": 0.8, "lr0": lr, "duration": duration, "runs": {}}
     if os.path.exists(path):
         prev = json.load(open(path))
-        if all(prev.get(k) == out[k] for k in ("steps", "omega0", "patience", "lr0")):
+        if all(prev.get(k, 1 if k == "duration" else None) == out[k]
+               for k in ("steps", "omega0", "patience", "lr0", "duration")):
             out["runs"] = prev["runs"]
     for s in seeds:
         if str(s) in out["runs"]:
@@ -355,6 +357,7 @@ def main():
     ap.add_argument("--patience", type=int, default=200)
     ap.add_argument("--lr", type=float, default=1e-3, help="--fullsize-seeds: Adam lr")
     ap.add_argument("--fullsize-file", default="trajectory_5x1024_w3000_seeds.json")
+    ap.add_argument("--duration", type=int, default=1, help="--fullsize-seeds: seconds of gt_bach")
     ap.add_argument("--seeds", default="0,1,2,3,4", help="init seeds of the multi-seed trajectories")
     ap.add_argument("--only-seeds", action="store_true", help="write only the multi-seed file")
     ap.add_argument("--only-act", action="store_true", help="write only the Snake / Tanh fixtures")
@@ -385,7 +388,8 @@ def main():
         return
     if args.fullsize_seeds:
         fullsize_seed_trajectories(ref_models, ref_utils, [int(s) for s in args.fullsize_seeds.split(",")],
-                                   args.trajectory_steps, args.patience, lr=args.lr, fname=args.fullsize_file)
+                                   args.trajectory_steps, args.patience, lr=args.lr, fname=args.fullsize_file,
+                                   duration=args.duration)
         return
     if args.only_seeds:
         seed_trajectories(ref_models, ref_utils, [int(s) for s in args.seeds.split(",")],

@@ -128,3 +128,99 @@ def test_train_kan_end_to_end(dev, tmp_path):
     assert params["arch"] == "kan" and np.isfinite(params["SNR"]) and np.isfinite(params["SNR_target"])
     sd = torch.load(ckpt, weights_only=True)["model_state_dict"]
     assert "layers.1.spline_scaler" in sd and "layers.0.grid" in sd
+
+
+def _torch_kanlinear(x, lay):
+    """kan.py:153-166 restated in plain torch fp64 (differentiable): SiLU base + B-spline term."""
+    from inr_for_audio_amd.kan import bspline_bases
+    xd = x.double()
+    base = torch.nn.functional.silu(xd) @ lay["base_weight"].t()
+    bases = bspline_bases(xd, lay["grid"], 3)
+    sw = lay["spline_weight"] * lay["spline_scaler"].unsqueeze(-1)
+    return base + bases.reshape(xd.shape[0], -1) @ sw.reshape(sw.shape[0], -1).t()
+
+
+def test_kan_autograd_vs_oracle(dev):
+    """KAN(...)(x) + loss.backward() (kan.py:268-273 in a user loop) through _KanFunction: the
+    parameter gradients equal the oracle's fp64 autograd of the same MSE (1e-4 relative L2)."""
+    m = _kan([1, 32, 48, 1])
+    sd = {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}
+    t, y = _data(2100)
+    m = m.to(dev)
+    out = m(torch.from_numpy(t).to(dev).reshape(1, -1, 1))
+    loss = torch.nn.MSELoss()(out, torch.from_numpy(y).to(dev).reshape(1, -1, 1))
+    loss.backward()
+    ref_out, xs = orc.kan_forward(sd, t, 3)
+    ref = orc.kan_backward(sd, xs, orc.mse_grad(ref_out, y), 3)
+    assert abs(float(loss) - orc.mse(ref_out, y)) < 1e-5 * orc.mse(ref_out, y)
+    for k, p in m.named_parameters():
+        r = ref[k]
+        rel = np.linalg.norm(p.grad.cpu().numpy().reshape(r.shape) - r) / np.linalg.norm(r)
+        assert rel < 1e-4, (k, rel)
+
+
+def test_kan_torch_optim_loop_matches_engine(dev):
+    """A hand-written torch.optim.Adam loop on the differentiable KAN follows the fused KanEngine
+    fit (same gradients, torch's Adam vs the device Adam kernel) and the oracle's Adam on the
+    oracle's fp64 gradients, over 6 steps."""
+    from inr_for_audio_amd.engine import KanEngine
+    widths, steps, lr = [1, 32, 32, 1], 6, 1e-3
+    t, y = _data(2100)
+    m = _kan(widths).to(dev)
+    sd0 = {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}
+    opt = torch.optim.Adam(m.parameters(), lr=lr)
+    x = torch.from_numpy(t).to(dev).reshape(1, -1, 1)
+    yt = torch.from_numpy(y).to(dev).reshape(1, -1, 1)
+    for _ in range(steps):
+        loss = torch.nn.MSELoss()(m(x), yt)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    eng = KanEngine(_kan(widths), torch.from_numpy(t), torch.from_numpy(y), lr=lr, device=dev)
+    for _ in range(steps):
+        eng.step()
+    got = {k: p.detach().cpu().numpy() for k, p in m.named_parameters()}
+    for i, k in enumerate(eng.layout.names):
+        e = eng.layout.view(eng.params, i).cpu().numpy()
+        d = np.linalg.norm(got[k] - e) / np.linalg.norm(e - sd0[k])
+        assert d < 1e-3, (k, d)  # relative to the distance the 6 steps moved the parameter
+    # oracle: its own gradients and Adam
+    sd = {k: v.astype(np.float64) for k, v in sd0.items()}
+    mom = {k: np.zeros_like(v) for k, v in sd.items() if not k.endswith("grid")}
+    vel = {k: np.zeros_like(v) for k, v in mom.items()}
+    for s in range(1, steps + 1):
+        o, xs = orc.kan_forward(sd, t, 3)
+        g = orc.kan_backward(sd, xs, orc.mse_grad(o, y), 3)
+        for k in mom:
+            sd[k], mom[k], vel[k] = orc.adam_step(sd[k], g[k], mom[k], vel[k], s, lr)
+    for k in mom:
+        d = np.linalg.norm(got[k] - sd[k]) / np.linalg.norm(sd[k] - sd0[k])
+        assert d < 1e-2, (k, d)
+
+
+@pytest.mark.parametrize("fin,fout", [(1, 16), (3, 5), (24, 70)])
+def test_kanlinear_alone_forward_backward(dev, fin, fout):
+    """A lone KANLinear (kan.py:153-166) is a module on the HIP path: output, parameter gradients
+    and the input gradient vs plain torch fp64 autograd of the same formula (70 outputs takes the
+    two-pass dW + dX kernels, <= 64 the one-pass kernel)."""
+    from inr_for_audio_amd.kan import KANLinear
+    torch.manual_seed(4)
+    lay = KANLinear(fin, fout)
+    ref_p = {k: v.detach().clone().double().requires_grad_(k != "grid") for k, v in lay.state_dict().items()}
+    x = torch.rand(3000, fin) * 2.4 - 1.2
+    xr = x.clone().double().requires_grad_(True)
+    out_ref = _torch_kanlinear(xr, ref_p)
+    w = torch.randn(3000, fout, dtype=torch.float64)
+    (out_ref * w).sum().backward()
+    lay = lay.to(dev)
+    xg = x.to(dev).requires_grad_(True)
+    out = lay(xg)
+    assert out.shape == (3000, fout)
+    assert float((out.double().cpu() - out_ref.detach()).abs().max()) < 1e-5 * max(1.0, float(out_ref.abs().max()))
+    (out * w.float().to(dev)).sum().backward()
+    for k, p in lay.named_parameters():
+        r = ref_p[k].grad
+        rel = float((p.grad.double().cpu() - r).norm() / r.norm())
+        assert rel < 1e-4, (k, rel)
+    rel = float((xg.grad.double().cpu() - xr.grad).norm() / xr.grad.norm())
+    assert rel < 1e-4, rel
