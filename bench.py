@@ -438,33 +438,16 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # BASELINE.md CPU plan: median of steps 2..k with torch.set_num_threads(os.cpu_count()).  On
         # the GPU box os.cpu_count() reports the whole host (256) while the job's CPU share is
-        # OMP_NUM_THREADS (16), and 256 threads on that share thrash (6x slower, measured): both
-        # counts are timed and the faster one is the reported value, the sweep kept beside it.
+        # OMP_NUM_THREADS (16), and 256 threads on that share thrash (6x slower, measured): the
+        # headline (cfg2) times both counts and reports the faster, the sweep kept beside it; the
+        # other configs time the share only (the thrashing leg costs minutes and never wins).
         from oracle import torch_cpu_step
-        cores = os.cpu_count() or 1
-        try:
-            affinity = len(os.sched_getaffinity(0))
-        except AttributeError:
-            affinity = cores
-        share = min(cores, int(os.environ.get("OMP_NUM_THREADS") or cores))
-        sweep = {}
-        for threads, steps in ((share, args.cpu_steps), (cores, max(3, args.cpu_steps // 2))):
-            if threads in sweep:
-                continue
-            cb = torch_cpu_step.time_steps(args.cpu_coords, H, L, steps=steps, threads=threads, omega0=omega0,
-                                           in_dim=in_dim)
-            sweep[threads] = cb
-        best_t = max(sweep, key=lambda k: sweep[k]["coord_samples_per_sec"])
-        cb = sweep[best_t]
-        result["cpu_baseline"] = {
-            "value": cb["coord_samples_per_sec"], "unit": "coord-samples/s", "cores": cb["threads"],
-            "kind": "port", "threads": cb["threads"], "cpu_count": cores, "affinity_cpus": affinity,
-            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-            "threads_sweep": {str(k): {"value": v["coord_samples_per_sec"], "steps": v["steps"],
-                                       "step_s": [round(x, 3) for x in v["step_times"]]} for k, v in sweep.items()},
-            "sample": f"torch-CPU fp32 port of run.py's step (oracle/torch_cpu_step.py), SIREN "
-                      f"{layers}x{H} (in = {in_dim}), {args.cpu_coords} coords, median of steps 2..k, "
-                      f"best of torch.set_num_threads({sorted(sweep)}) (os.cpu_count() = {cores}), {cpu_model()}"}
+        what = (f"torch-CPU fp32 port of run.py's step (oracle/torch_cpu_step.py), SIREN {layers}x{H} "
+                f"(in = {in_dim}), {args.cpu_coords} coords")
+        result["cpu_baseline"] = cpu_baseline_sweep(
+            lambda threads, steps: torch_cpu_step.time_steps(args.cpu_coords, H, L, steps=steps, threads=threads,
+                                                             omega0=omega0, in_dim=in_dim),
+            args, what, share_only=args.config != "cfg2")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

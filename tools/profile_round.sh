@@ -31,8 +31,8 @@ python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_lds.json" "$OUT/pmc_lds" &&
 python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_hbm.json" "$OUT/pmc_fetch" "$OUT/pmc_write" &&
 python3 "$ROOT/tools/pmc_mfma.py" "$OUT/bench_pmc_mfma.json" "$OUT/pmc_mfma" &&
 for c in cfg3 cfg4 cfg5; do
-  CB=--no-cpu-baseline; [ $c = cfg5 ] && CB=   # cfg5 carries its own (KAN) CPU port
-  timeout -k 10 300 python3 "$ROOT/bench.py" --config $c $CB > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" &&
+  # every config line carries its CPU baseline (cfg3 / cfg4: the SIREN port at the job's thread share)
+  timeout -k 10 300 python3 "$ROOT/bench.py" --config $c > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" &&
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$c" -o run -- \
     python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/trace_$c.log" 2>&1 || exit 3
 done

@@ -63,7 +63,56 @@ _FL_NEW = """if constexpr (SN == 4 && MODE == NT_FWD) {
           }
         }"""
 
+# forward epilogue stores through buffer descriptors of the wave's 128-row band (base in SGPRs,
+# one 32-bit lane offset, the row subtile in soffset) instead of 64-bit per-lane addresses
+_BST_OLD1 = """      float hp[SM];
+#pragma unroll
+      for (int j = 0; j < SM; ++j) hp[j] = 0.f;"""
+_BST_NEW1 = """      float hp[SM];
+#pragma unroll
+      for (int j = 0; j < SM; ++j) hp[j] = 0.f;
+      const size_t obase = (size_t)(m0 + wm * TM) * N + n0;
+      const auto rsy = __builtin_amdgcn_make_buffer_rsrc(p.Y + obase, (short)0, TM * N * 2, 0x00020000);
+      const auto rsc = __builtin_amdgcn_make_buffer_rsrc(p.C + obase, (short)0, TM * N * 2, 0x00020000);
+      const int qv = ((lane & 15) * N + wn * TN + swap16_col(lane)) * 2;
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));"""
+_BST_OLD2 = """          st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
+          st16(p.C + rowoff + npc + pp * 32, cpk[pp]);"""
+_BST_NEW2 = """          if constexpr (MODE == NT_FWD) {
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{yp[pp].x, yp[pp].y, yp[pp].z, yp[pp].w}, rsy, qv + pp * 64,
+                                                   j * 16 * N * 2, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{cpk[pp].x, cpk[pp].y, cpk[pp].z, cpk[pp].w}, rsc,
+                                                   qv + pp * 64, j * 16 * N * 2, 0);
+          } else {
+            st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
+            st16(p.C + rowoff + npc + pp * 32, cpk[pp]);
+          }"""
+
+# the forward epilogue's pre-activation as packed fp32 FMAs (v_pk_fma_f32: two per instruction)
+_PK_OLD = """#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
+                // hardware sin/cos inside their reduced domain for any magnitude.
+                const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
+                s[r] = __builtin_amdgcn_sinf(x);
+                c[r] = __builtin_amdgcn_cosf(x);
+              }"""
+_PK_NEW = """typedef float f32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+              for (int r = 0; r < 4; r += 2) {
+                const f32x2 z2 = __builtin_elementwise_fma(f32x2{acc[i][j][r], acc[i][j][r + 1]}, f32x2{xs, xs},
+                                                           f32x2{bb[r], bb[r + 1]});
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                  const float x = __builtin_amdgcn_fractf(z2[q]);
+                  s[r + q] = __builtin_amdgcn_sinf(x);
+                  c[r + q] = __builtin_amdgcn_cosf(x);
+                }
+              }"""
+
 VARIANTS = {
+    "pkfma": {"gemm_nt.hip": [(_PK_OLD, _PK_NEW)]},
+    "bst": {"gemm_nt.hip": [(_BST_OLD1, _BST_NEW1), (_BST_OLD2, _BST_NEW2)]},
     "st_sc1": {"gemm_nt.hip": [(_ST16, _st16_asm("sc1"))]},          # write-through epilogue stores
     "st_nt": {"gemm_nt.hip": [(_ST16, _st16_asm("nt"))]},            # non-temporal epilogue stores
     "st_sc0sc1": {"gemm_nt.hip": [(_ST16, _st16_asm("sc0 sc1"))]},
