@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 8
+#define SIREN_ABI_VERSION 9
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 /* ints in one tile-queue counter set (siren_batch.tileq, siren_inner_fwd's tileq): the
@@ -207,6 +207,25 @@ int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float
 int siren_inner_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, float omega, int32_t rows,
                     int32_t hidden, uint16_t* Y, uint16_t* C, const float* head_w, float* head_part,
                     int32_t* tileq, void* stream);
+/* siren_train_step's fused last layer (SIREN_OPT_HEAD_FUSE): models.py:114-115 hidden SineLayer,
+ * the head (models.py:374-381), MSELoss / L1Loss gradient (run.py:161-169, loss_mode as
+ * siren_batch) and the head backward in one launch -- out, g = dLoss/d(head linear output),
+ * 256-row sse / gsum partials (as siren_head_loss), dZ = dZ_L x gscale[0] (as siren_head_bwd) and
+ * part[rows/256][2][hidden] = column partials of db_L and dw_head.  Y / C are not written.  Needs
+ * rows % 256 == 0 and the 256x256 ping-pong NT tiles (else SIREN_ERR_CONFIG); head_part is
+ * [hidden/256][rows] scratch. */
+int siren_head_fused_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, float omega, int32_t rows,
+                         int32_t hidden, const float* w_head, const float* b_head, float head_omega, const float* y,
+                         int32_t n_valid, double n_total, int32_t loss_mode, const float* gscale, float* head_part,
+                         float* out, float* g, float* sse_part, float* gsum_part, uint16_t* dZ, float* part,
+                         void* stream);
+/* the fused head's backward scale, fixed before the forward: gscale = {S, 1/S} from a bound of
+ * max|g| (MSE: (sum|w_head| + |b_head| + max|y|) 2/n_total, or 1 + max|y| through a final sine of
+ * head_omega; L1: 1/n_total; x head_omega) x max|w_head| x act_bound (|dY/dz| bound of the last
+ * layer); max|y| over the n_valid target rows, ymax_part = (n_valid+255)/256 floats of scratch */
+int siren_grad_scale_bound(const float* y, int32_t n_valid, float* ymax_part, const float* w_head,
+                           const float* b_head, int32_t hidden, double n_total, float head_omega, int32_t loss_mode,
+                           float act_bound, float* gscale, void* stream);
 /* any inner layer kind: SINE as siren_inner_fwd; SNAKE (models.py:235-241): z = X W^T + b,
  * Y = z + sin^2(a z)/a, C = 1 + sin(2az), E = (z sin(2az) - sin^2(az)/a)/a; TANH
  * (models.py:366-372): Y = tanh z, C = 1 - Y^2 (a, E unused) */
@@ -352,7 +371,10 @@ enum siren_prof_kind {
    * backward) and the first layer's weight gradient (+ slab reduces); KAN_DX the hidden layers'
    * one-pass backward (dW and dX); KAN_MISC the small rest */
   SIREN_PROF_KAN_FWD = 8, SIREN_PROF_KAN_DW = 9, SIREN_PROF_KAN_DX = 10, SIREN_PROF_KAN_MISC = 11,
-  SIREN_PROF_NKINDS = 12
+  /* the last hidden layer fused with the head, the loss gradient and the head backward
+   * (siren_train_step with SIREN_OPT_HEAD_FUSE; counted apart from INNER_FWD) */
+  SIREN_PROF_HEAD_FWD = 12,
+  SIREN_PROF_NKINDS = 13
 };
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
  * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;
@@ -373,10 +395,14 @@ enum siren_prof_kind {
  * from the caller's tile-queue set (siren_batch.tileq; 8 shard heads, agent-scope atomics) in the
  * forward modes, 2: in every mode, 0: never (the static walk b, b + G, ...).  Results are
  * identical.  (Options 5 and 7, the round-2 start stagger and X L2-prefetch distance, were
- * measured neutral or slower and retired with their kernels: they return SIREN_ERR_CONFIG.) */
+ * measured neutral or slower and retired with their kernels: they return SIREN_ERR_CONFIG.)
+ * SIREN_OPT_HEAD_FUSE = 1 (default): siren_train_step runs a sine last layer on 256x256
+ * ping-pong tiles as one launch with the head, the loss gradient and the head backward
+ * (dZ_L is written instead of Y_L / C_L; the backward scale S then comes from a bound of
+ * max|g| known before the forward); 0: separate forward, head_loss and head_bwd launches. */
 enum siren_option {
   SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1, SIREN_OPT_NT_PIPE = 2, SIREN_OPT_TN_PIPE = 3,
-  SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_DIAG = 6, SIREN_OPT_NT_QUEUE = 8
+  SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_DIAG = 6, SIREN_OPT_NT_QUEUE = 8, SIREN_OPT_HEAD_FUSE = 9
 };
 int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);

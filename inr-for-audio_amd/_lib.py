@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_INNER = 16
 ROW_TILE = 128
 TILEQ_INTS = 768  # SIREN_TILEQ_INTS: one tile-queue counter set
@@ -148,6 +148,10 @@ _SIGS = {
     "siren_adam_step": (ctypes.c_int, [_p, _p, _p, _p, _i64, _p, _p]),
     "siren_plateau_step": (ctypes.c_int, [_p, _p, ctypes.c_double, _p, _p, _i64, _p]),
     "siren_cast_weight": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p]),
+    "siren_head_fused_fwd": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, ctypes.c_float, _p, _i32,
+                                            ctypes.c_double, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "siren_grad_scale_bound": (ctypes.c_int, [_p, _i32, _p, _p, _p, _i32, ctypes.c_double, ctypes.c_float, _i32,
+                                              ctypes.c_float, _p, _p]),
     "siren_set_option": (ctypes.c_int, [_i32, _i32]),
     "siren_fp32_linear": (ctypes.c_int, [_p, _i64, _i32, _i32, _p, _p, ctypes.c_float, _p, _p]),
     "siren_fp32_act": (ctypes.c_int, [_i32, _p, _i64, _i32, _p, _p, _p]),
@@ -170,7 +174,7 @@ _SIGS = {
 STRUCTS = [SirenNet, SirenGrads, SirenBatch, SirenOptState, SirenKanNet, SirenKanGrads, SirenKanBatch, SirenGuard]
 
 PROF_KINDS = ["first_fwd", "inner_fwd", "head", "bwd_dw", "bwd_dx", "bwd_dx0", "reduce", "update",
-              "kan_fwd", "kan_dw", "kan_dx", "kan_misc"]
+              "kan_fwd", "kan_dw", "kan_dx", "kan_misc", "head_fwd"]
 
 
 def profile_read() -> dict:

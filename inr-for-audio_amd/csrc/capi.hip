@@ -110,8 +110,15 @@ inline hipError_t mark_ready(const siren_batch* b, int k, hipStream_t s) {
   return b->grad_ready[k] ? hipEventRecord((hipEvent_t)b->grad_ready[k], s) : hipSuccess;
 }
 
-// forward through all layers + head partials; returns hip status
-hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s) {
+// SIREN_OPT_HEAD_FUSE: siren_train_step runs the last layer as NT_FWD_HB when it can
+int g_head_fuse = 1;
+bool head_fused(const siren_net* n, const siren_batch* b) {
+  return g_head_fuse && n->act[n->n_inner - 1] == SIREN_ACT_SINE && gemm_nt_head_fusable(b->rows, n->hidden);
+}
+
+// forward through all layers + head partials; returns hip status.  hb: the last layer is the
+// fused NT_FWD_HB (training; gfac = the loss gradient factor, b->gscale already set)
+hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s, bool hb = false, float gfac = 0.f) {
   const int R = b->rows, H = n->hidden, L = n->n_inner;
   SIREN_PROF(SIREN_PROF_FIRST_FWD, s, first_fwd(b->coords, n->in_dim, n->W0, n->b0, n->omega0, R, H, B(b->Y[0]),
                                                 B(b->C[0]), s, n->first_snake ? n->a0 : nullptr,
@@ -132,6 +139,14 @@ hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s) {
     p.head_w = n->w_head;
     p.head_part = b->head_part;
     p.tileq = b->tileq;
+    if (head && hb) {
+      p.target = b->target; p.b_head = n->b_head; p.out = b->out; p.g = b->g;
+      p.sse_part = b->sse_part; p.gsum_part = b->gsum_part;
+      p.n_valid = b->n_valid; p.loss_mode = b->loss_mode; p.gfac = gfac; p.head_omega = n->head_omega;
+      p.gscale = b->gscale; p.dZ = B(b->dZ[0]); p.colsum_part = b->col_part;
+      SIREN_PROF(SIREN_PROF_HEAD_FWD, s, gemm_nt(NT_FWD_HB, true, p, s));
+      continue;
+    }
     SIREN_PROF(SIREN_PROF_INNER_FWD, s, gemm_nt(fwd_mode(n->act[i]), head, p, s));
   }
   return hipSuccess;
@@ -213,23 +228,30 @@ static int check_grads(const siren_net* net, const siren_grads* gr) {
   return SIREN_OK;
 }
 
-// autograd of models.py:388-394 given dLoss/dout in batch->g (rows >= n_valid are zero)
-static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch* b, hipStream_t s) {
+// autograd of models.py:388-394 given dLoss/dout in batch->g (rows >= n_valid are zero).  hb: the
+// forward's NT_FWD_HB already wrote dZ_L and the [R/256][2][H] partials of db_L and dw_head
+static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch* b, hipStream_t s,
+                        bool hb = false) {
   const int R = b->rows, H = net->hidden, L = net->n_inner, in = net->in_dim;
   const int ntile = nt_choose_tile(R, H), tntile = tn_choose_tile(R, H, H);
   const int prow = R / ntile;  // partial rows written by the NT_DX / NT_DX0 epilogues
-  const bool snake_last = net->act[L - 1] == SIREN_ACT_SNAKE;
-  float* da_last = b->col_part + (int64_t)(R / 128) * H;  // second H-wide slab of col_part
-  SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale(b->gmax_part, (R + 255) / 256, net->w_head, H,
-                                            act_bound(net, L - 1), b->gscale, s,
-                                            (const GuardState*)b->guard));
-  SIREN_PROF(SIREN_PROF_HEAD, s, head_bwd(B(b->C[L]), B(b->Y[L]), b->g, net->w_head, act_omega(net, L - 1),
-                                          R, H, b->gscale, B(b->dZ[0]), b->col_part, b->col_part2,
-                                          snake_last ? B(b->E[L]) : nullptr, snake_last ? da_last : nullptr, s));
-  SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part2, H, R / 128, H, gr->w_head, 1, 1, b->red_tmp, s));
-  SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, R / 128, H, gr->b[L - 1], 1, 1, b->red_tmp, s));
-  if (snake_last)
-    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(da_last, H, R / 128, H, gr->a[L - 1], 1, 1, b->red_tmp, s));
+  if (hb) {
+    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + H, 2 * H, prow, H, gr->w_head, 1, 1, b->red_tmp, s));
+    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, 2 * H, prow, H, gr->b[L - 1], 1, 1, b->red_tmp, s));
+  } else {
+    const bool snake_last = net->act[L - 1] == SIREN_ACT_SNAKE;
+    float* da_last = b->col_part + (int64_t)(R / 128) * H;  // second H-wide slab of col_part
+    SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale(b->gmax_part, (R + 255) / 256, net->w_head, H,
+                                              act_bound(net, L - 1), b->gscale, s,
+                                              (const GuardState*)b->guard));
+    SIREN_PROF(SIREN_PROF_HEAD, s, head_bwd(B(b->C[L]), B(b->Y[L]), b->g, net->w_head, act_omega(net, L - 1),
+                                            R, H, b->gscale, B(b->dZ[0]), b->col_part, b->col_part2,
+                                            snake_last ? B(b->E[L]) : nullptr, snake_last ? da_last : nullptr, s));
+    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part2, H, R / 128, H, gr->w_head, 1, 1, b->red_tmp, s));
+    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, R / 128, H, gr->b[L - 1], 1, 1, b->red_tmp, s));
+    if (snake_last)
+      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(da_last, H, R / 128, H, gr->a[L - 1], 1, 1, b->red_tmp, s));
+  }
   SIREN_TRY(mark_ready(b, L + 1, s));  // head: w_head, b_head (and sse, summed before the backward)
 
   int cur = 0;
@@ -300,18 +322,29 @@ int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b
 
   if (b->zero_grads && gr->flat) SIREN_TRY(hipMemsetAsync(gr->flat, 0, gr->flat_len * sizeof(float), s));
 
-  // ---- forward (models.py:388-394) + MSE / L1 (run.py:161-169) ----
-  SIREN_TRY(run_forward(net, b, s));
   // mean backward: MSELoss 2 err / N, L1Loss sign(err) / N
   const float gfac = (float)((b->loss_mode == 1 ? 1.0 : 2.0) / b->n_total);
-  SIREN_PROF(SIREN_PROF_HEAD, s, head_loss(b->head_part, H / nt_choose_tile(R, H), R, net->b_head,
-                                           b->target, b->n_valid, gfac, b->out, b->g, b->sse_part,
-                                           b->gsum_part, b->gmax_part, s, net->head_omega, b->loss_mode));
+  const bool hb = head_fused(net, b);
+  if (hb) {
+    // the fused head needs the backward scale S before the forward: from the bound of max|g|
+    // (elementwise.hip grad_scale_bound) instead of the step's max|g|
+    const int L = net->n_inner, nv = b->n_valid, nyp = (nv + 255) / 256;
+    if (nv > 0) SIREN_PROF(SIREN_PROF_HEAD, s, gmax_partials(b->target, nv, b->gmax_part, s));
+    SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale_bound(b->gmax_part, nyp, net->w_head, net->b_head, H, gfac,
+                                                    net->head_omega, b->loss_mode, act_bound(net, L - 1),
+                                                    b->gscale, s, (const GuardState*)b->guard));
+  }
+  // ---- forward (models.py:388-394) + MSE / L1 (run.py:161-169) ----
+  SIREN_TRY(run_forward(net, b, s, hb, gfac));
+  if (!hb)
+    SIREN_PROF(SIREN_PROF_HEAD, s, head_loss(b->head_part, H / nt_choose_tile(R, H), R, net->b_head,
+                                             b->target, b->n_valid, gfac, b->out, b->g, b->sse_part,
+                                             b->gsum_part, b->gmax_part, s, net->head_omega, b->loss_mode));
   const int nsum = (R + 255) / 256;
   SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->sse_part, nsum, gr->sse, 1, s));
   SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->gsum_part, nsum, gr->b_head, 1, s));
   // ---- backward (autograd of run.py:185) ----
-  return run_backward(net, gr, b, s);
+  return run_backward(net, gr, b, s, hb);
 }
 
 int siren_backward(const siren_net* net, const siren_grads* gr, siren_batch* b, void* stream) {
@@ -414,6 +447,41 @@ int siren_head_bwd(const uint16_t* C, const uint16_t* Y, const float* g, const f
   if (!hidden_ok(hidden) || rows <= 0 || rows % SIREN_ROW_TILE) return SIREN_ERR_SHAPE;
   return (int)head_bwd(B(C), B(Y), g, w_head, omega, rows, hidden, gscale, B(dZ), db_part, dwh_part,
                        B(E), da_part, S(stream));
+}
+
+int siren_head_fused_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, float omega, int32_t rows,
+                         int32_t hidden, const float* w_head, const float* b_head, float head_omega, const float* y,
+                         int32_t n_valid, double n_total, int32_t loss_mode, const float* gscale, float* head_part,
+                         float* out, float* g, float* sse_part, float* gsum_part, uint16_t* dZ, float* part,
+                         void* stream) {
+  if (!X || !Wh || !b || !w_head || !b_head || !gscale || !head_part || !out || !g || !sse_part || !gsum_part ||
+      !dZ || !part || (n_valid > 0 && !y))
+    return SIREN_ERR_NULL;
+  if (!hidden_ok(hidden) || rows <= 0 || rows % 256 || n_valid < 0 || n_valid > rows || !(n_total > 0))
+    return SIREN_ERR_SHAPE;
+  if (loss_mode < 0 || loss_mode > 1 || !(head_omega >= 0.f)) return SIREN_ERR_CONFIG;
+  if (!gemm_nt_head_fusable(rows, hidden)) return SIREN_ERR_CONFIG;
+  NtParams p = {};
+  p.X = B(X); p.W = B(Wh); p.M = rows; p.N = hidden; p.K = hidden;
+  p.tile = nt_choose_tile(rows, hidden);
+  p.omega = omega; p.bias = b; p.head_w = w_head; p.head_part = head_part;
+  p.target = y; p.b_head = b_head; p.out = out; p.g = g; p.sse_part = sse_part; p.gsum_part = gsum_part;
+  p.n_valid = n_valid; p.loss_mode = loss_mode; p.gfac = (float)((loss_mode == 1 ? 1.0 : 2.0) / n_total);
+  p.head_omega = head_omega; p.gscale = gscale; p.dZ = B(dZ); p.colsum_part = part;
+  return (int)gemm_nt(NT_FWD_HB, true, p, S(stream));
+}
+
+int siren_grad_scale_bound(const float* y, int32_t n_valid, float* ymax_part, const float* w_head,
+                           const float* b_head, int32_t hidden, double n_total, float head_omega, int32_t loss_mode,
+                           float act_bound, float* gscale, void* stream) {
+  if (!w_head || !b_head || !gscale || (n_valid > 0 && (!y || !ymax_part))) return SIREN_ERR_NULL;
+  if (n_valid < 0 || hidden < 1 || !(n_total > 0)) return SIREN_ERR_SHAPE;
+  if (loss_mode < 0 || loss_mode > 1) return SIREN_ERR_CONFIG;
+  hipStream_t s = S(stream);
+  if (n_valid > 0) SIREN_TRY(gmax_partials(y, n_valid, ymax_part, s));
+  return (int)grad_scale_bound(ymax_part, (n_valid + 255) / 256, w_head, b_head, hidden,
+                               (float)((loss_mode == 1 ? 1.0 : 2.0) / n_total), head_omega, loss_mode, act_bound,
+                               gscale, s);
 }
 
 int siren_inner_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, int32_t act,
@@ -588,6 +656,10 @@ int siren_set_option(int32_t option, int32_t value) {
     case SIREN_OPT_NT_QUEUE:
       if (value < 0 || value > 2) return SIREN_ERR_CONFIG;
       gemm_nt_set_queue(value);
+      return SIREN_OK;
+    case SIREN_OPT_HEAD_FUSE:
+      if (value < 0 || value > 1) return SIREN_ERR_CONFIG;
+      g_head_fuse = value;
       return SIREN_OK;
   }
   return SIREN_ERR_CONFIG;

@@ -277,6 +277,53 @@ __global__ void grad_scale_kernel(const float* __restrict__ gmax_part, int npart
   }
 }
 
+// S for the fused head backward (NT_FWD_HB), fixed BEFORE the forward, so it cannot use the step's
+// max|g|.  Instead it bounds it from quantities known then: MSE g = (out - y) * gfac with
+// |out| <= sum|w_head| * max|Y_L| + |b_head| (max|Y_L| <= 1 for a sine / tanh last layer; 1 for
+// the final sine of last_linear=False), L1 |g| <= gfac, times head_omega through the final sine.
+// The bound is loose by ~sum|w_head| / max|out - y| (2^4-2^5 at H = 1024), which only moves
+// dZ_L x S further below the fp16 maximum (scaling by a power of two is exact above fp16's
+// normal minimum).  ymax_part: per-256-row max|target| partials (gmax_partials on the target).
+__global__ void grad_scale_bound_kernel(const float* __restrict__ ymax_part, int nparts,
+                                        const float* __restrict__ w_head, const float* __restrict__ b_head, int H,
+                                        float gfac, float head_omega, int loss_mode, float act_bound,
+                                        float* __restrict__ gscale, const GuardState* __restrict__ guard) {
+  __shared__ float scratch[4];
+  float ym = 0.f, wm = 0.f, ws = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) ym = fmaxf(ym, ymax_part[i]);
+  for (int i = threadIdx.x; i < H; i += blockDim.x) {
+    const float a = fabsf(w_head[i]);
+    wm = fmaxf(wm, a);
+    ws += a;
+  }
+  ym = block_max(ym, scratch);
+  wm = block_max(wm, scratch);
+  ws = block_sum(ws, scratch);
+  if (threadIdx.x == 0) {
+    float gb = loss_mode == 1 ? gfac : gfac * ((head_omega > 0.f ? 1.0f : ws + fabsf(b_head[0])) + ym);
+    if (head_omega > 0.f) gb *= head_omega;
+    // 2^-10 of slack over the fp32 roundings of the bound itself
+    const float bound = gb * wm * fabsf(act_bound) * (1.0f + 0x1p-10f);
+    int k = 0;
+    if (bound > 0.f && bound < INFINITY) {
+      int e;
+      (void)frexpf(bound, &e);
+      k = (guard ? guard->headroom : kHeadroomDefault) - e;
+      k = k < -100 ? -100 : (k > 100 ? 100 : k);
+    }
+    gscale[0] = ldexpf(1.0f, k);
+    gscale[1] = ldexpf(1.0f, -k);
+  }
+}
+
+hipError_t grad_scale_bound(const float* ymax_part, int nparts, const float* w_head, const float* b_head, int H,
+                            float gfac, float head_omega, int loss_mode, float act_bound, float* gscale,
+                            hipStream_t s, const GuardState* guard) {
+  hipLaunchKernelGGL(grad_scale_bound_kernel, dim3(1), dim3(256), 0, s, ymax_part, nparts, w_head, b_head, H, gfac,
+                     head_omega, loss_mode, act_bound, gscale, guard);
+  return hipGetLastError();
+}
+
 hipError_t grad_scale(const float* gmax_part, int nparts, const float* w_head, int H, float omega,
                       float* gscale, hipStream_t s, const GuardState* guard) {
   hipLaunchKernelGGL(grad_scale_kernel, dim3(1), dim3(256), 0, s, gmax_part, nparts, w_head, H, omega,

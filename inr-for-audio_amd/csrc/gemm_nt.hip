@@ -114,12 +114,15 @@ static_assert(kQueueSet == kTileqInts, "siren_hip.h SIREN_TILEQ_INTS");
 
 constexpr bool nt_is_dx0(int m) { return m == NT_DX0 || m == NT_DX0_SNAKE; }
 
+// NT_FWD_HB: head_part word not yet published by its column tile's block (launch_nt fills it)
+constexpr unsigned kHeadPending = 0xFFFFFFFFu;
+
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
 constexpr int epilogue_stores() {
   return (MODE == NT_FWD || MODE == NT_FWD_TANH) ? Cfg::SM * Cfg::SN
          : MODE == NT_FWD_SNAKE                 ? 3 * Cfg::SM * Cfg::SN / 2
-         : (MODE == NT_DX || MODE == NT_DX_SNAKE) ? Cfg::SM * Cfg::SN / 2
+         : (MODE == NT_DX || MODE == NT_DX_SNAKE || MODE == NT_FWD_HB) ? Cfg::SM * Cfg::SN / 2
                                                   : 0;
 }
 
@@ -268,7 +271,176 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     const int npc = n0 + wn * TN + swap16_col(lane);      // swapped layout: this lane's piece
     const int mrow0 = m0 + wm * TM + (lane & 15);
 
-    if constexpr (nt_is_fwd(MODE)) {
+    if constexpr (MODE == NT_FWD_HB) {
+      // ---- phase 1: Y = sin, C = cos of the tile rounded to fp16 as NT_FWD stores them, packed
+      // IN PLACE of their accumulators (4 fp32 -> 4 + 4 fp16: the same 4 VGPRs, so nothing more is
+      // live across the hand-off than the accumulators themselves), and the head partial of the
+      // band's rows over this column tile, summed exactly as NT_FWD + HEAD sums it
+      const int nq = n0 + wn * TN + 4 * (lane >> 4);
+      const float xs = p.omega * kInv2Pi;
+      float4 bias[SN], hw[SN];
+#pragma unroll
+      for (int i = 0; i < SN; ++i) {
+        const float4 b = *(const float4*)(bias_lds + nq + i * 16);
+        bias[i] = float4{b.x * xs, b.y * xs, b.z * xs, b.w * xs};
+        hw[i] = *(const float4*)(hw_lds + nq + i * 16);
+      }
+      float hp[SM];
+#pragma unroll
+      for (int j = 0; j < SM; ++j) {
+        hp[j] = 0.f;
+#pragma unroll
+        for (int q = 0; q < SN / 2; ++q) {
+          const int pp = (Cfg::PP && j >= SM / 2) ? SN / 2 - 1 - q : q;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * pp + h;
+            const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
+            float sv[4], cv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
+              sv[r] = __builtin_amdgcn_sinf(x);
+              cv[r] = __builtin_amdgcn_cosf(x);
+            }
+            const uint2 yv = as_u2(pack4(sv[0], sv[1], sv[2], sv[3])), cw = as_u2(pack4(cv[0], cv[1], cv[2], cv[3]));
+            acc[i][j] = __builtin_bit_cast(f32x4, uint4{yv.x, yv.y, cw.x, cw.y});
+            // opaque: the packing happens here (left to itself the compiler sinks the cos past the
+            // hand-off into phase 2, keeping the fp32 arguments live across it: 372 B of spills)
+            asm volatile("" : "+v"(acc[i][j]));
+            hp[j] += sv[0] * hw[i].x + sv[1] * hw[i].y + sv[2] * hw[i].z + sv[3] * hw[i].w;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < SM; ++j) {
+        hp[j] += __shfl_xor(hp[j], 16, 64);
+        hp[j] += __shfl_xor(hp[j], 32, 64);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < SM; ++j) red[wn * BM + wm * TM + j * 16 + lane] = hp[j];
+      }
+      lds_barrier();
+      // ---- the band hand-off: publish this column tile's partial of each row, take the other
+      // column tiles' partials as their blocks publish them (the band's tiles_n tiles run in
+      // lockstep on tiles_n consecutive blocks of one XCD; DESIGN §4 "fused head backward"), then
+      // head_loss for the band's rows.  The partial itself is the flag: head_part is filled with
+      // kHeadPending before the launch and a published value is never that pattern (NaN is
+      // stored canonical), so no fence orders it -- one agent-scope atomic word each way.
+      float* g_lds = red + WN * BM;
+      float e2 = 0.f, gv = 0.f;
+      if (tid < BM) {
+        float own = 0.f;
+#pragma unroll
+        for (int w = 0; w < WN; ++w) own += red[w * BM + tid];
+        const int m = m0 + tid;
+        unsigned* hpu = (unsigned*)p.head_part;
+        __hip_atomic_store(hpu + (size_t)tn * p.M + m, own == own ? __float_as_uint(own) : 0x7fc00000u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float o = 0.f;  // head_loss_kernel's order: partials j = 0, 1, ..., then the bias
+        for (int jt = 0; jt < tiles_n; ++jt) {
+          float v = own;
+          if (jt != tn) {
+            unsigned u;
+            while ((u = __hip_atomic_load(hpu + (size_t)jt * p.M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
+                   kHeadPending)
+              __builtin_amdgcn_s_sleep(1);
+            v = __uint_as_float(u);
+          }
+          o += v;
+        }
+        o += p.b_head[0];
+        const float a = p.head_omega * o;
+        const float ov = p.head_omega > 0.f ? sinf(a) : o;
+        if (m < p.n_valid) {
+          const float err = ov - p.target[m];
+          if (p.loss_mode == 1) {
+            e2 = fabsf(err);
+            gv = (err > 0.f ? 1.0f : (err < 0.f ? -1.0f : 0.f)) * p.gfac;
+          } else {
+            e2 = err * err;
+            gv = err * p.gfac;
+          }
+          if (p.head_omega > 0.f) gv = (gv * cosf(a)) * p.head_omega;
+        }
+        g_lds[tid] = gv;
+        if (tn == 0) {
+          p.out[m] = ov;
+          p.g[m] = gv;
+        }
+      }
+      // the band's loss and bias-gradient partials (head_loss_kernel's 256-row blocks and sums;
+      // threads >= BM add zeros); the block sums' barriers also publish g_lds
+      const float se = block_sum(e2, g_lds + BM);
+      const float gs = block_sum(gv, g_lds + BM);
+      if (tn == 0 && tid == 0) {
+        p.sse_part[tm] = se;
+        p.gsum_part[tm] = gs;
+      }
+      // ---- phase 2: head_bwd_kernel on the registers: dz = ((g w) C) omega stored x S, column
+      // partials of dz (db_L) and of g Y (dw_head) over the tile's rows
+      // column pairs outermost (the 16-B dZ pieces pair adjacent subtiles), rows inside: each
+      // pair's accumulators and column partials die before the next pair's begin
+      const float om = p.omega, S = p.gscale[0];
+      float gm[SM];
+#pragma unroll
+      for (int j = 0; j < SM; ++j) gm[j] = g_lds[wm * TM + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int pp = 0; pp < SN / 2; ++pp) {
+        float cs[2][2][4];  // [db_L, dw_head][subtile h][column r]
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[q][h][r] = 0.f;
+#pragma unroll
+        for (int j = 0; j < SM; ++j) {
+          uint2 dzp[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * pp + h;
+            const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);
+            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+            const uint4 pk = __builtin_bit_cast(uint4, acc[i][j]);
+            const h16x4 yh = as_h4(uint2{pk.x, pk.y}), ch = as_h4(uint2{pk.z, pk.w});
+            float d[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float c = (float)ch[r], y = (float)yh[r];
+              const float dz = ((gm[j] * wv[r]) * c) * om;
+              cs[0][h][r] += dz;
+              cs[1][h][r] += gm[j] * y;
+              d[r] = dz * S;
+            }
+            dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
+          }
+          st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[q][h][r]);
+            if ((lane & 15) == 0)
+              *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + (2 * pp + h) * 16 + 4 * (lane >> 4)) =
+                  float4{v[0], v[1], v[2], v[3]};
+          }
+      }
+      lds_barrier();
+      if (tid < BN) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          float sum = 0.f;
+#pragma unroll
+          for (int w = 0; w < Cfg::WM; ++w) sum += red[(q * Cfg::WM + w) * BN + tid];
+          p.colsum_part[((size_t)tm * 2 + q) * N + n0 + tid] = sum;
+        }
+      }
+    } else if constexpr (nt_is_fwd(MODE)) {
       const int nq = n0 + wn * TN + 4 * (lane >> 4);     // natural layout: this lane's columns
       const float xs = (MODE == NT_FWD) ? p.omega * kInv2Pi : 1.0f;
       float4 bias[SN], hw[SN];
@@ -622,7 +794,23 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
   // the queue's shards are blockIdx % 8: every shard must have blocks
   // (measured: the forward gains 3-4%; dX is unchanged and dX0 loses 2%, its K-loop spills)
   const bool want = g_nt_queue == 2 || (g_nt_queue == 1 && nt_is_fwd(MODE));
-  if constexpr (Cfg::PP) {
+  if constexpr (MODE == NT_FWD_HB) {
+    // the static walk g = bp + i G with G a multiple of tiles_n: the tiles_n column tiles of a row
+    // band are tile i of tiles_n consecutive blocks (one XCD under the xcd_remap order), which wait
+    // for each other's head partials.  Blocks are dispatched in order, so a waiting block's
+    // partners are resident or next in line (at most tiles_n - 1 blocks per XCD wait on blocks
+    // not yet dispatched while every fully resident band group runs on).
+    static_assert(Cfg::PP, "fused head: ping-pong persistent walk");
+    const int tiles_n = p.N / Cfg::BN;
+    if (p.diag || tiles_n > 4 || p.M % Cfg::BM) return hipErrorInvalidValue;
+    int g = grid - grid % tiles_n;
+    if (g < tiles_n) g = tiles_n;
+    const hipError_t e = hipMemsetAsync(p.head_part, 0xFF, (size_t)tiles_n * p.M * sizeof(float), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD>), dim3(g), dim3(Cfg::THREADS), 0, s, p);
+    return hipGetLastError();
+  }
+  if constexpr (Cfg::PP && MODE != NT_FWD_HB) {
     if (p.tileq && want && !p.diag && grid % 8 == 0) {
       // the counter set starts every launch at zero, ordered on the launch's own stream
       // (graph capture records the memset as a node before the kernel)
@@ -685,8 +873,19 @@ int nt_choose_tile(int M, int N) {
   return (long)(M / 256) * (N / 256) >= 512 ? 256 : 128;
 }
 
+bool gemm_nt_head_fusable(int M, int N) {
+  return nt_choose_tile(M, N) == 256 && nt_pp() && M % 256 == 0 && N % 256 == 0 && N / 256 <= 4 && N % 128 == 0;
+}
+
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (p.M % NtSmall::BM || p.N % NtSmall::BN || p.K % NtSmall::BK || p.M <= 0 || p.N > NtSmall::MAXN) return hipErrorInvalidValue;
+  if (mode == NT_FWD_HB) {
+    if (!head || p.tile != 256 || !gemm_nt_head_fusable(p.M, p.N)) return hipErrorInvalidValue;
+    if (!p.head_w || !p.head_part || !p.gscale || !p.dZ || !p.colsum_part || !p.b_head || !p.out || !p.g ||
+        !p.sse_part || !p.gsum_part || (p.n_valid > 0 && !p.target))
+      return hipErrorInvalidValue;
+    return launch_nt<NtLargePP, NT_FWD_HB, true>(p, s, true);
+  }
   if (nt_is_dx0(mode) && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
   if (mode == NT_DX0_SNAKE) {
     if (!p.Eprev) return hipErrorInvalidValue;

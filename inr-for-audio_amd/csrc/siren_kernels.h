@@ -12,9 +12,11 @@ typedef _Float16 h16;  // activation / weight-shadow / gradient storage (fp16, s
 // a Snake layer (derivative D and d/da E of the layer below), SURVEY §8 f3
 // NT_DX0_SNAKE: dX into a Linear + Snake first layer (first_linear=True): dz = acc * D0, partials
 // of db0, dW0 (x t_j) and da0 = sum acc * E0
+// NT_FWD_HB: the last hidden SineLayer fused with the head, the loss gradient and the head backward
+// (training only): writes dZ_L x S instead of Y_L / C_L (see gemm_nt.hip)
 enum NtMode { NT_FWD = 0, NT_DX = 1, NT_DX0 = 2, NT_FWD_SNAKE = 3, NT_FWD_TANH = 4, NT_DX_SNAKE = 5,
-              NT_DX0_SNAKE = 6 };
-constexpr bool nt_is_fwd(int m) { return m == NT_FWD || m == NT_FWD_SNAKE || m == NT_FWD_TANH; }
+              NT_DX0_SNAKE = 6, NT_FWD_HB = 7 };
+constexpr bool nt_is_fwd(int m) { return m == NT_FWD || m == NT_FWD_SNAKE || m == NT_FWD_TANH || m == NT_FWD_HB; }
 
 struct NtParams {
   const h16* X;  // [M][K]
@@ -45,11 +47,24 @@ struct NtParams {
   // ping-pong K-loop only: caller-owned tile-queue counter set of kTileqInts ints (null = the
   // static walk b, b + G, ...); gemm_nt zeroes it on the stream before each queue launch
   int* tileq;
+  // NT_FWD_HB (with head_w / head_part; gscale = {S, 1/S} set beforehand by grad_scale_bound;
+  // dZ = dZ_L x S; colsum_part [M/256][2][N] = partials of db_L and dw_head): head_loss's inputs
+  // and outputs for the band's rows
+  const float* target;  // [M]
+  const float* b_head;  // [1]
+  float* out;           // [M]
+  float* g;             // [M] dLoss/d(head linear output)
+  float* sse_part;      // [M/256]
+  float* gsum_part;     // [M/256]
+  int n_valid, loss_mode;
+  float gfac, head_omega;
 };
 constexpr int kTileqInts = 768;  // == SIREN_TILEQ_INTS (include/siren_hip.h)
 
 int nt_choose_tile(int M, int N);
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s);
+// NT_FWD_HB is available for this shape under the current tile / K-loop settings
+bool gemm_nt_head_fusable(int M, int N);
 void gemm_nt_set_tile(int tile);  // 0 = auto, 128, 256 (A/B measurement)
 void gemm_tn_set_tile(int tile);
 void gemm_nt_set_pipe(int v);     // 256x256 K-loop: 4 ping-pong (default), 1 persistent, 0 one tile per block
@@ -102,6 +117,11 @@ hipError_t head_loss(const float* head_part, int nparts, int R, const float* b_h
 hipError_t gmax_partials(const float* g, int R, float* gmax_part, hipStream_t s);
 hipError_t head_sine_chain(const float* head_part, int nparts, int R, const float* b_head, float omega, float* g,
                            hipStream_t s);
+// S before the forward (NT_FWD_HB): from a loss-independent bound of max|g| -- ymax_part holds
+// (n_valid+255)/256 max|target| partials; act_bound = |dY/dz| bound of the last layer
+hipError_t grad_scale_bound(const float* ymax_part, int nparts, const float* w_head, const float* b_head, int H,
+                            float gfac, float head_omega, int loss_mode, float act_bound, float* gscale,
+                            hipStream_t s, const GuardState* guard = nullptr);
 // gscale[0] = S (dZ storage scale), gscale[1] = 1/S; from (R+255)/256 max|g| partials
 hipError_t grad_scale(const float* gmax_part, int nparts, const float* w_head, int H, float omega,
                       float* gscale, hipStream_t s, const GuardState* guard = nullptr);

@@ -65,6 +65,33 @@ def grad_scale(g: np.ndarray, wf: np.ndarray, omega: float, headroom: int = 6) -
     return math.ldexp(1.0, int(min(max(headroom - e, -100), 100)))
 
 
+def grad_scale_bound(y: np.ndarray, n_valid: int, wf: np.ndarray, bf: float, n_total: float, act_bound: float,
+                     head_omega: float = 0.0, loss_mode: int = 0, headroom: int = 6) -> float:
+    """elementwise.hip grad_scale_bound_kernel -- the backward scale of siren_train_step's fused
+    head (gemm_nt.hip NT_FWD_HB), fixed before the forward from a bound of max|g|:
+    MSE gfac ((head_omega > 0 ? 1 : sum|w_head| + |b_head|) + max|y|), L1 gfac, times head_omega
+    through a final sine; times max|w_head| |act_bound| (1 + 2^-10), then S = 2^(headroom-e) as
+    grad_scale.  A different power-of-two S changes no stored dZ bit unless a value leaves fp16's
+    normal range, so the oracle's default (grad_scale of the step's max|g|) agrees with the fused
+    path to within subnormal rounding; tests of the fused path pass this S to backward(scale=)."""
+    gfac = F32((1.0 if loss_mode == 1 else 2.0) / n_total)
+    yv = np.abs(np.asarray(y, F32).reshape(-1)[:n_valid])
+    ym = F32(yv.max()) if yv.size else F32(0)
+    wa = np.abs(np.asarray(wf, F32).reshape(-1))
+    wm, ws = F32(wa.max()), F32(wa.astype(F64).sum())
+    if loss_mode == 1:
+        gb = gfac
+    else:
+        gb = F32(gfac * F32((F32(1) if head_omega > 0 else F32(ws + F32(abs(float(bf))))) + ym))
+    if head_omega > 0:
+        gb = F32(gb * F32(head_omega))
+    bound = F32(F32(F32(gb * wm) * F32(abs(act_bound))) * F32(1.0 + 2.0 ** -10))
+    if not (bound > 0 and np.isfinite(bound)):
+        return 1.0
+    _, e = math.frexp(float(bound))
+    return math.ldexp(1.0, int(min(max(headroom - e, -100), 100)))
+
+
 def fma32(a, b, c) -> np.ndarray:
     """fp32 fused multiply-add: a*b is exact in fp64, one rounding of the sum to fp32
     (double rounding through fp64 differs from a true fma in < 2^-29 of cases)."""
@@ -253,11 +280,12 @@ def mse(out: np.ndarray, y: np.ndarray) -> float:
 
 
 def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float, omega: float,
-             half: bool = False, dtype=F64, headroom: int = 6) -> dict:
+             half: bool = False, dtype=F64, headroom: int = 6, scale: float | None = None) -> dict:
     """Autograd of the SIREN for upstream dLoss/dout = g [N].  Returns a dict of grads in
     nn.Linear layout (same keys as Params.to_state_dict).  With `half`, every dZ_i is
     rounded as the HIP path stores it: fp16(dZ_i * S) / S (exact power-of-two scale, S from
-    grad_scale with the given `headroom`)."""
+    grad_scale with the given `headroom`, or `scale` when given: grad_scale_bound's S of the
+    fused head)."""
     L = len(p.W)
     Y, A, C, E = cache["Y"], cache["A"], cache["C"], cache.get("E", [None] * (L + 1))
     layers, (hw, hb) = p.keys()
@@ -266,7 +294,7 @@ def backward(p: Params, t: np.ndarray, cache: dict, g: np.ndarray, omega0: float
         g = (np.asarray(g, F64) * np.cos(p.head_omega * o) * p.head_omega).astype(F32)
     # backward scale bound: |dY/dz| of the last layer (elementwise.hip grad_scale / capi act_bound)
     bound = {"sine": omega, "snake": 2.0, "tanh": 1.0}[p.kinds[-1]]
-    S = grad_scale(g, p.wf, bound, headroom) if half else 1.0
+    S = (scale if scale is not None else grad_scale(g, p.wf, bound, headroom)) if half else 1.0
     g = np.asarray(g, dtype).reshape(-1)
     grads = {}
     grads[hw] = (g @ np.asarray(Y[L], dtype)).reshape(1, -1)

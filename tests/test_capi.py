@@ -44,7 +44,7 @@ def test_struct_layouts_match(lib):
 
 
 def test_host_only_helpers(lib):
-    assert lib.siren_abi_version() == 8
+    assert lib.siren_abi_version() == 9
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256
@@ -91,15 +91,17 @@ def test_set_option_ranges(lib):
     """siren_set_option validates every knob on the host (SIREN_OPT_* in siren_hip.h) and leaves
     the defaults restored; SIREN_OPT_NT_QUEUE takes 0 (static walk), 1 (forward modes), 2 (all).
     The product library carries no measurement ablation: SIREN_OPT_NT_DIAG accepts only 0, and
-    the retired stagger (5) and prefetch-distance (7) options are rejected."""
+    the retired stagger (5) and prefetch-distance (7) options are rejected; SIREN_OPT_HEAD_FUSE (9)
+    takes 0 or 1."""
     bad = 1003  # SIREN_ERR_CONFIG
     for opt, good, wrong in ((0, (0, 128, 256), (64,)), (1, (0, 128, 256), (512,)), (2, (-1, 0, 1, 4), (2, 3, 5, 7, -2)),
                              (3, (-1, 4), (5,)), (4, (0, 16), (-1,)), (5, (), (0, 1)),
-                             (6, (0,), (1, 4, 512, 1024, 2, 8)), (7, (), (1, 2)), (8, (0, 1, 2), (3, -1))):
+                             (6, (0,), (1, 4, 512, 1024, 2, 8)), (7, (), (1, 2)), (8, (0, 1, 2), (3, -1)),
+                             (9, (0, 1), (2, -1))):
         for v in good:
             assert lib.siren_set_option(opt, v) == 0, (opt, v)
         for v in wrong:
             assert lib.siren_set_option(opt, v) == bad, (opt, v)
     assert lib.siren_set_option(99, 0) == bad
-    for opt, v in ((0, 0), (1, 0), (2, -1), (3, -1), (4, 0), (6, 0), (8, 1)):
+    for opt, v in ((0, 0), (1, 0), (2, -1), (3, -1), (4, 0), (6, 0), (8, 1), (9, 1)):
         assert lib.siren_set_option(opt, v) == 0

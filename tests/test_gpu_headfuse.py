@@ -1,0 +1,188 @@
+"""The fused head backward (gemm_nt.hip NT_FWD_HB; SIREN_OPT_HEAD_FUSE, default on).
+
+siren_train_step runs a sine last layer, the head (models.py:374-381), the MSE / L1 gradient
+(run.py:161-169) and the head backward as ONE launch: the column tiles of a row band run in
+lockstep on consecutive blocks and hand their head partials to each other (DESIGN §4 "fused
+head backward").  Checked against the unfused launches (SIREN_OPT_HEAD_FUSE 0: the same loss,
+outputs and dLoss/dout bit for bit, gradients to fp32 summation order) and against the oracle
+with the fused path's backward scale (grad_scale_bound).  The NT tile is forced to 256 so that
+4k-8k-row cases take the path; small persistent grids make every block walk many bands."""
+import numpy as np
+import pytest
+import torch
+
+from errlog import check_grads, log
+from oracle import siren_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+OPT_NT_TILE, OPT_NT_GRID, OPT_HEAD_FUSE = 0, 4, 9
+DEFAULTS = {OPT_NT_TILE: 0, OPT_NT_GRID: 0, OPT_HEAD_FUSE: 1}
+
+
+@pytest.fixture
+def opts(lib):
+    touched = []
+
+    def set_(o, v):
+        assert lib.siren_set_option(o, v) == 0, (o, v)
+        touched.append(o)
+
+    yield set_
+    for o in touched:
+        lib.siren_set_option(o, DEFAULTS[o])
+
+
+def _engine(dev, H, L, n, *, w0=3000.0, ll=True, loss="mse", mb=1 << 20, seed=0):
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(seed)
+    model = SirenWithSnakeTanh(1, 1, H, L, 0, 0, last_linear=ll, first_omega_0=w0, hidden_omega_0=30.0)
+    sd0 = {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    t = torch.linspace(-1, 1, n).reshape(n, 1)
+    y = 0.5 * torch.sin(37 * t) + 0.3 * torch.sin(91 * t + 0.5)
+    eng = SirenEngine(model, t, y, micro_batch=mb, loss_mode=loss, device=dev)
+    return eng, sd0, t, y
+
+
+def _grads(eng, lib):
+    """One siren_train_step per micro-batch (no update); (grads, out, g, per-kind launches)."""
+    from inr_for_audio_amd import _lib
+    _lib.check(lib.siren_profile_enable(64 * eng.n_micro), "profile_enable")
+    eng._launch_grads()
+    torch.cuda.synchronize()
+    prof = _lib.profile_read()
+    _lib.check(lib.siren_profile_enable(0), "profile_disable")
+    return eng.grads.clone(), eng.ws.out.clone(), eng.ws.g.clone(), {k: n for k, (_, n) in prof.items()}
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.mark.parametrize("H,L,n,grid,ll,loss,mb", [
+    (1024, 4, 8192, 0, True, "mse", 1 << 20),    # 4 column tiles per band, 32 bands on 128 blocks
+    (1024, 4, 8192, 8, True, "mse", 1 << 20),    # 2 band groups walking 16 bands each
+    (1024, 4, 8000, 12, True, "mse", 1 << 20),   # pad rows (g = 0), 3 band groups
+    (512, 3, 4096, 6, True, "mae", 1 << 20),     # L1Loss, 2 column tiles per band
+    (256, 2, 4096, 0, False, "mse", 1 << 20),    # last_linear=False (final sine), 1 tile per band
+    (1024, 2, 6000, 4, True, "mse", 2048),       # 3 micro-batches accumulating
+])
+def test_fused_matches_unfused(dev, lib, opts, H, L, n, grid, ll, loss, mb):
+    opts(OPT_NT_TILE, 256)
+    opts(OPT_NT_GRID, grid)
+    eng, _, _, _ = _engine(dev, H, L, n, ll=ll, loss=loss, mb=mb)
+    ga, oa, gga, ka = _grads(eng, lib)
+    opts(OPT_HEAD_FUSE, 0)
+    gb, ob, ggb, kb = _grads(eng, lib)
+    # the fused path ran (one launch per micro-batch, no head_loss / head_bwd), the other did not
+    assert ka["head_fwd"] == eng.n_micro and kb["head_fwd"] == 0
+    assert ka["inner_fwd"] == (L - 1) * eng.n_micro and kb["inner_fwd"] == L * eng.n_micro
+    assert ka["head"] == 2 * eng.n_micro and kb["head"] == 3 * eng.n_micro
+    # head_loss's arithmetic on the same head partials: bit-identical outputs, dLoss/dout, loss
+    assert torch.equal(oa, ob) and torch.equal(gga, ggb)
+    sse = eng.layout.sse_offset
+    assert torch.equal(ga[sse], gb[sse])
+    lay = eng.layout
+    errs = {k: _rel(lay.view(ga, i), lay.view(gb, i)) for i, k in enumerate(lay.names)}
+    log(f"headfuse_vs_unfused[{H}x{L}x{n}x{grid}x{ll}x{loss}x{mb}]", errs=errs)
+    # only the S of the dZ storage (a different power of two: bits differ only below fp16's normal
+    # range) and the fp32 order of the db_L / dw_head column sums differ
+    for k, e in errs.items():
+        assert e < 2e-5, (k, e)
+
+
+@pytest.mark.parametrize("H,L,n,ll,loss", [
+    (1024, 4, 4000, True, "mse"),
+    (512, 3, 4096, True, "mae"),
+    (256, 2, 4096, False, "mse"),
+])
+def test_fused_vs_oracle(dev, lib, opts, H, L, n, ll, loss):
+    opts(OPT_NT_TILE, 256)
+    eng, sd0, t, y = _engine(dev, H, L, n, ll=ll, loss=loss)
+    got_g, _, _, kinds = _grads(eng, lib)
+    assert kinds["head_fwd"] == 1
+    p = orc.Params.from_state_dict(sd0, L, 0, 0, False, ll)
+    S = orc.grad_scale_bound(y.numpy(), n, p.wf, float(np.asarray(p.bf).reshape(-1)[0]), n, 30.0,
+                             head_omega=p.head_omega, loss_mode=1 if loss == "mae" else 0)
+    assert float(eng.ws.gscale[0]) == S and float(eng.ws.gscale[1]) == 1.0 / S
+    out, cache = orc.forward(p, t.numpy(), 3000.0, 30.0, half=True, dtype=np.float64)
+    gl = orc.l1_grad(out, y.numpy()) if loss == "mae" else orc.mse_grad(out, y.numpy())
+    ref = orc.backward(p, t.numpy(), cache, gl, 3000.0, 30.0, half=True, scale=S)
+    got = {k: eng.layout.view(got_g, i).cpu().numpy() for i, k in enumerate(eng.layout.names)}
+    check_grads(f"headfuse_vs_oracle[{H}x{L}x{n}x{ll}x{loss}]", got, ref)
+    lref = orc.l1(out, y.numpy()) if loss == "mae" else orc.mse(out, y.numpy())
+    lgot = float(got_g[eng.layout.sse_offset]) / n
+    assert abs(lgot - lref) <= 1e-4 * lref, (lgot, lref)
+
+
+def test_fused_step_graph_and_determinism(dev, opts):
+    """Eager steps, a captured step replayed, and a second engine: bit-identical parameters and
+    losses (the hand-off's partial order is fixed, so no run-to-run drift)."""
+    opts(OPT_NT_TILE, 256)
+    a, _, _, _ = _engine(dev, 1024, 3, 8192)
+    b, _, _, _ = _engine(dev, 1024, 3, 8192)
+    for _ in range(4):
+        a.step()
+    b.step()
+    b.capture_graph()
+    for _ in range(3):
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params)
+    la, _ = a.history()
+    lb, _ = b.history()
+    assert np.array_equal(la, lb)
+
+
+@pytest.mark.parametrize("H,R,n_valid,grid", [
+    (1024, 4096, 4096, 0),
+    (1024, 4096, 3000, 8),    # pad rows; 2 band groups walking 8 bands each
+    (512, 2048, 2048, 2),
+    (256, 2048, 1500, 0),
+])
+def test_kernel_vs_unfused_launches(dev, lib, opts, H, R, n_valid, grid):
+    """siren_head_fused_fwd against siren_inner_fwd (+ head) -> siren_head_loss -> siren_head_bwd
+    with the same backward scale: outputs, dLoss/dout, the 256-row loss partials and the stored
+    dZ_L bit-identical; the db_L / dw_head column partials (256- instead of 128-row blocks) agree
+    to fp32 summation order."""
+    import ctypes
+    from inr_for_audio_amd._lib import new_tileq
+    opts(OPT_NT_TILE, 256)
+    opts(OPT_NT_GRID, grid)
+    g_ = torch.Generator(device=dev).manual_seed(H + R)
+    f16 = torch.float16
+    P = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+    s = torch.cuda.current_stream().cuda_stream
+    X = torch.sin(torch.rand(R, H, device=dev, generator=g_) * 6.2831853).to(f16)
+    W = ((torch.rand(H, H, device=dev, generator=g_) * 2 - 1) * (6 / H) ** 0.5 / 30).to(f16)
+    b = (torch.rand(H, device=dev, generator=g_) - 0.5) * 0.06
+    wh = (torch.rand(H, device=dev, generator=g_) - 0.5) * 2 / H ** 0.5
+    bh = torch.tensor([0.01], device=dev)
+    y = (torch.rand(R, device=dev, generator=g_) - 0.5)
+    gs = torch.tensor([2.0 ** 9, 2.0 ** -9], device=dev)
+    e = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
+    hp1, out1, g1, sse1, gsum1, dZ1, part1 = e(H // 256, R), e(R), e(R), e(R // 256), e(R // 256), e(R, H, dt=f16), \
+        e(R // 256, 2, H)
+    st = lib.siren_head_fused_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(wh), P(bh), ctypes.c_float(0.0),
+                                  P(y), n_valid, float(n_valid), 0, P(gs), P(hp1), P(out1), P(g1), P(sse1), P(gsum1),
+                                  P(dZ1), P(part1), s)
+    assert st == 0, lib.siren_status_string(st)
+    Y, C, hp2 = e(R, H, dt=f16), e(R, H, dt=f16), e(H // 256, R)
+    out2, g2, sse2, gsum2, dZ2 = e(R), e(R), e(R // 256), e(R // 256), e(R, H, dt=f16)
+    db2, dw2 = e(R // 128, H), e(R // 128, H)
+    tq = new_tileq(dev)
+    for st in (lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(Y), P(C), P(wh), P(hp2), P(tq), s),
+               lib.siren_head_loss(P(hp2), H // 256, R, P(bh), P(y), n_valid, float(n_valid), P(out2), P(g2), P(sse2),
+                                   P(gsum2), None, s),
+               lib.siren_head_bwd(P(C), P(Y), P(g2), P(wh), ctypes.c_float(30.0), R, H, P(gs), P(dZ2), P(db2), P(dw2),
+                                  None, None, s)):
+        assert st == 0, lib.siren_status_string(st)
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2) and torch.equal(g1, g2)
+    assert torch.equal(sse1, sse2) and torch.equal(gsum1, gsum2)
+    assert torch.equal(dZ1, dZ2)
+    for got, ref in ((part1[:, 0].double().sum(0), db2.double().sum(0)), (part1[:, 1].double().sum(0),
+                                                                          dw2.double().sum(0))):
+        assert float((got - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) + 1e-12

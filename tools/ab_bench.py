@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--hidden", type=int, default=1024)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--only", default="fwd,fwd_head,dx,dx0,dw", help="cases")
+    ap.add_argument("--only", default="fwd,fwd_head,fwd_hb,dx,dx0,dw", help="cases")
     args = ap.parse_args()
     from inr_for_audio_amd import _lib
     libs = {}
@@ -53,7 +53,12 @@ def main():
     # zero-filled: the parity check compares whole buffers, including what a tile size leaves unwritten
     outs = {nm: {"Y": torch.zeros(R, H, dtype=f16, device=dev), "C": torch.zeros(R, H, dtype=f16, device=dev),
                  "hp": torch.zeros(H // 128, R, device=dev), "dZp": torch.zeros(R, H, dtype=f16, device=dev),
-                 "part": torch.zeros(R // 128, 3, H, device=dev)} for nm in libs}
+                 "part": torch.zeros(R // 128, 3, H, device=dev), "out": torch.zeros(R, device=dev),
+                 "g": torch.zeros(R, device=dev), "sse": torch.zeros(R // 256, device=dev),
+                 "gsum": torch.zeros(R // 256, device=dev)} for nm in libs}
+    y = torch.sin(t[:, 0] * 2300.0) * 0.5
+    bh = torch.zeros(1, device=dev)
+    gs = torch.tensor([2.0 ** 9, 2.0 ** -9], device=dev)
     tq = _lib.new_tileq(dev)
     splits = list(libs.values())[0].siren_default_splits(R, H)
     slab = torch.empty(int(list(libs.values())[0].siren_slab_floats(H, splits)), device=dev)
@@ -67,6 +72,11 @@ def main():
         if kind == "fwd_head":
             return lambda: lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(o["Y"]), P(o["C"]),
                                                P(hw), P(o["hp"]), P(tq), s())
+        if kind == "fwd_hb":  # the fused last layer + head + MSE gradient + head backward
+            return lambda: lib.siren_head_fused_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(hw), P(bh),
+                                                    ctypes.c_float(0.0), P(y), R, float(R), 0, P(gs), P(o["hp"]),
+                                                    P(o["out"]), P(o["g"]), P(o["sse"]), P(o["gsum"]), P(o["dZp"]),
+                                                    P(o["part"]), s())
         if kind == "dx":
             return lambda: lib.siren_inner_bwd_dx(P(dZ), P(WT), P(Cp), ctypes.c_float(30.0), R, H, None,
                                                   P(o["dZp"]), P(o["part"]), s())
@@ -96,7 +106,7 @@ def main():
                 torch.cuda.synchronize()
                 o = outs[nm]
                 got[nm] = {"fwd": (o["Y"], o["C"]), "fwd_head": (o["Y"], o["C"], o["hp"]), "dx": (o["dZp"], o["part"]),
-                           "dx0": (o["part"],)}[k]
+                           "dx0": (o["part"],), "fwd_hb": (o["out"], o["g"], o["sse"], o["dZp"], o["part"])}[k]
                 got[nm] = tuple(x.clone() for x in got[nm])
             for nm in libs:
                 if nm != base:

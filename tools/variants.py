@@ -110,7 +110,15 @@ _PK_NEW = """typedef float f32x2 __attribute__((ext_vector_type(2)));
                 }
               }"""
 
+# fused head (NT_FWD_HB) cost split: no hand-off (each block uses its own partial for all column
+# tiles: WRONG g, timing only)
+_HB_WAIT_OLD = """            while ((u = __hip_atomic_load(hpu + (size_t)jt * p.M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
+                   kHeadPending)
+              __builtin_amdgcn_s_sleep(1);"""
+_HB_WAIT_NEW = """            u = __float_as_uint(own) + jt;"""
+
 VARIANTS = {
+    "hb_nowait": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW)]},
     "pkfma": {"gemm_nt.hip": [(_PK_OLD, _PK_NEW)]},
     "bst": {"gemm_nt.hip": [(_BST_OLD1, _BST_NEW1), (_BST_OLD2, _BST_NEW2)]},
     "st_sc1": {"gemm_nt.hip": [(_ST16, _st16_asm("sc1"))]},          # write-through epilogue stores
