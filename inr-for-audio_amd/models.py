@@ -15,6 +15,7 @@ eager fallback: CPU tensors or unsupported configurations raise.
 from __future__ import annotations
 
 import ctypes
+import math
 
 import numpy as np
 import torch
@@ -346,7 +347,15 @@ class _Fp32Act(torch.autograd.Function):
         rows = xs.numel() // cols
         y = torch.empty_like(xs)
         s = torch.cuda.current_stream(x.device).cuda_stream
-        ac = None if a is None else a.detach().reshape(-1).contiguous().float()
+        ac = None
+        ctx.a_shape = None
+        if a is not None:
+            # the kernel reads a[column]: one value per column, or a scalar broadcast to every column
+            # (the reference's Snake broadcasts `a` against x; models.py:241)
+            if a.numel() not in (1, cols):
+                raise ValueError(f"Snake a has {a.numel()} values for {cols} columns (need {cols} or 1)")
+            ac = a.detach().reshape(-1).float().expand(cols).contiguous()
+            ctx.a_shape = a.shape
         _lib.check(lib.siren_fp32_act(int(act), _lib.ptr(xs), rows, cols, _lib.ptr(ac), _lib.ptr(y), s),
                    "siren_fp32_act")
         ctx.save_for_backward(xs, ac if ac is not None else torch.empty(0, device=x.device))
@@ -369,6 +378,8 @@ class _Fp32Act(torch.autograd.Function):
         _lib.check(lib.siren_fp32_act_bwd(ctx.act, _lib.ptr(xs), rows, cols, _lib.ptr(ac if ctx.has_a else None),
                                           _lib.ptr(g), _lib.ptr(gx), _lib.ptr(da), _lib.ptr(prod), _lib.ptr(tmp), s),
                    "siren_fp32_act_bwd")
+        if da is not None:  # back to a's own shape (summed over the columns a scalar a was broadcast to)
+            da = (da.sum() if math.prod(ctx.a_shape) == 1 and cols > 1 else da).reshape(ctx.a_shape)
         return gx, None, da
 
 

@@ -358,6 +358,8 @@ def main():
     ap.add_argument("--lr", type=float, default=1e-3, help="--fullsize-seeds: Adam lr")
     ap.add_argument("--fullsize-file", default="trajectory_5x1024_w3000_seeds.json")
     ap.add_argument("--duration", type=int, default=1, help="--fullsize-seeds: seconds of gt_bach")
+    ap.add_argument("--clip", type=int, default=0, help="write only gt_bach_<clip>s.npz: the WaveformFitting "
+                    "target of the first <clip> seconds (the data of the --duration fixtures)")
     ap.add_argument("--seeds", default="0,1,2,3,4", help="init seeds of the multi-seed trajectories")
     ap.add_argument("--only-seeds", action="store_true", help="write only the multi-seed file")
     ap.add_argument("--only-act", action="store_true", help="write only the Snake / Tanh fixtures")
@@ -369,6 +371,10 @@ def main():
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 1)
     ref_models, ref_utils = import_reference()
+    if args.clip:
+        _, target = ref_utils.WaveformFitting(os.path.join(REF, "gt_bach.wav"), duration=args.clip, decimation=1)[0]
+        np.savez_compressed(os.path.join(OUT, f"gt_bach_{args.clip}s.npz"), target=target.numpy().reshape(-1))
+        return
     if args.only_multiwave:
         multiwave_fixtures(ref_utils)
         checkpoint_fixture(ref_models, ref_utils)

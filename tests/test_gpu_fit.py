@@ -10,7 +10,8 @@ summation order on the same seed moves it by as much -- DESIGN.md "Fit parity").
   * fit quality is compared as statistics over init seeds 0-7 against the reference's
     own runs of the same seeds: the median over seeds of the best-loss SNR
     10 log10(var(target) / min_k loss_k) -- the error floor each run reaches, insensitive
-    to where a spike happens to fall -- within north_star's 0.1 dB.  The final SNR is a much
+    to where a spike happens to fall -- within north_star's 0.1 dB plus the fp32 reference's
+    own summation-order sensitivity on this fixture (a fixed 0.25 dB, BOUND_3X256).  The final SNR is a much
     noisier statistic: bootstrapping the reference's 8 seeds gives its median a 5.5 dB
     standard deviation (7.8 dB for a difference of two such medians), so it is only checked
     one-sided at two standard deviations, GPU median >= reference median - 15 dB (a broken
@@ -20,8 +21,10 @@ summation order on the same seed moves it by as much -- DESIGN.md "Fit parity").
 The headline model itself (SIREN 5x1024, omega0 = 3000) has its own fixture: the reference's
 run of 200 full-batch steps on gt_bach 1 s for 4 seeds (lr 1e-4 -- at run.py's 1e-3 this width
 does not leave the init plateau in 200 steps -- and patience 10, so ReduceLROnPlateau drops
-the lr inside the run).  Same 0.1 dB gate on the best-loss median, identical lr schedules
-while they track, and no fp16 overflow step.
+the lr inside the run).  The best-loss median within a fixed 2.1 dB (BOUND_5X1024_CHAOTIC: at lr
+1e-4 the fp32 reference itself moves 1.97 dB with its summation order), identical lr schedules
+while they track, and no fp16 overflow step.  North_star's 0.1 dB is held PER SEED in the stable
+regime (lr 3e-5) on gt_bach 1 s and on 6 s (264 600 coordinates, across a plateau lr drop).
 """
 import json
 import os
@@ -73,12 +76,15 @@ def _torch_gpu_best(dev, var, seed, steps, H=256, L=2, w0=1000.0, lr=1e-3, patie
     return _db(var, np.min(losses)), int(np.sum(np.diff(lrs) < 0))
 
 
-def _envelope(ours, ref, t32):
-    """|ours - ref| must stay within 0.1 dB of the distance between two fp32 runs of the
-    reference algorithm itself (CPU fixture vs torch eager on this GPU): on these chaotic
-    full-batch fits the fp32 reference moves by that much when only its summation order
-    changes (DESIGN.md "Fit parity")."""
-    return abs(ours - ref) < 0.1 + abs(t32 - ref)
+# Fixed bounds on |median over seeds of the GPU's best-loss SNR - the reference's| (dB) for the two
+# chaotic multi-seed fixtures: north_star's 0.1 dB plus the fp32 reference algorithm's own
+# sensitivity to summation order on that fixture, measured ONCE as |median(torch fp32 eager on the
+# GPU) - median(CPU reference)| over the fixture's seeds (r11: 0.15 dB for 3x256 over 8 seeds;
+# 1.97 dB for the 5x1024 lr 1e-4 run over 4 seeds).  The torch fp32 runs are still made and
+# logged, but no longer widen the gate.  The per-seed 0.1 dB gates are the stable-regime tests
+# (1 s and 6 s) at the end of this file.
+BOUND_3X256 = 0.25
+BOUND_5X1024_CHAOTIC = 2.1
 
 
 def test_fit_first_steps_track_reference(dev):
@@ -118,7 +124,7 @@ def test_fit_quality_vs_reference_over_seeds(dev):
           f"\nfinal SNR median:     GPU {med(fin_gpu):.2f} dB, reference {med(fin_ref):.2f} dB"
           f"\nper seed GPU  best {np.round(best_gpu, 2).tolist()} final {np.round(fin_gpu, 2).tolist()}"
           f"\nper seed ref  best {np.round(best_ref, 2).tolist()} final {np.round(fin_ref, 2).tolist()}")
-    assert _envelope(med(best_gpu), med(best_ref), med(best_t32))
+    assert abs(med(best_gpu) - med(best_ref)) < BOUND_3X256
     assert med(fin_gpu) >= med(fin_ref) - 15.0
     assert abs(med(tail_gpu) - med(tail_ref)) < 11.0
 
@@ -160,7 +166,7 @@ def test_fit_quality_headline_model_over_seeds(dev):
     print(f"\n5x1024 best-loss SNR median: GPU {med(best_gpu):.2f} dB, reference {med(best_ref):.2f} dB; "
           f"lr drops GPU {drops_gpu} reference {drops_ref}")
     assert drops_ref > 0 and drops_gpu > 0
-    assert _envelope(med(best_gpu), med(best_ref), med(best_t32))
+    assert abs(med(best_gpu) - med(best_ref)) < BOUND_5X1024_CHAOTIC
 
 
 def test_fit_headline_model_stable_regime_per_seed(dev):
@@ -190,3 +196,62 @@ def test_fit_headline_model_stable_regime_per_seed(dev):
         assert abs(v["final_snr_gpu"] - v["final_snr_ref"]) < 0.1, (s, v)
         assert abs(v["best_gpu"] - v["best_ref"]) < 0.1, (s, v)
         assert v["max_step_db"] < 0.1, (s, v)
+
+
+def _fit6(dev, steps, seed, patience, lr):
+    """SIREN 5x1024, omega0 3000, on gt_bach 6 s (264 600 coordinates: a quarter of cfg2's 2^20
+    rows, the longest whole-second clip of the reference's gt_bach.wav): the fused path with
+    its production settings (256 tiles, fused head backward, graph replay)."""
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    from inr_for_audio_amd.utils import calculate_snr, get_coord
+    target = np.load(os.path.join(G, "gt_bach_6s.npz"))["target"]
+    coords = get_coord(target.size, 1).reshape(-1, 1)
+    torch.manual_seed(seed)
+    m = SirenWithSnakeTanh(1, 1, 1024, 4, 0, 0, first_omega_0=3000.0, hidden_omega_0=30.0)
+    eng = SirenEngine(m, coords, torch.from_numpy(target), lr=lr, min_lr=1e-6, patience=patience, hist_cap=steps,
+                      device=dev)
+    assert eng.lib.siren_nt_tile(eng.rows, 1024) == 256
+    eng.step()
+    eng.capture_graph()
+    while eng.steps_applied() < steps:
+        eng.step()
+    assert eng.guard_state()["overflows"] == 0
+    out = eng.infer(coords.to(dev)).cpu().numpy()
+    return eng, float(calculate_snr(target, out)), float(np.mean(target.astype(np.float64) ** 2))
+
+
+@pytest.mark.parametrize("fixture", ["trajectory_5x1024_w3000_lr3e-5_6s_seeds.json",
+                                     "trajectory_5x1024_w3000_lr3e-5_6s_p3.json"])
+def test_fit_headline_model_6s_per_seed(dev, fixture):
+    """cfg2's model on cfg2-scale data: SIREN 5x1024, omega0 3000, gt_bach 6 s,
+    60 full-batch steps at lr 3e-5 per seed against the reference's own runs (make_golden.py
+    --fullsize-seeds --duration 6).  The _p3 fixture lowers the plateau patience to 3 so the run
+    crosses a ReduceLROnPlateau drop.  Per seed: the lr trace is identical, every step's loss is
+    within STEP_DB of the reference's, and the final and best-loss SNR within north_star's 0.1 dB."""
+    ref = json.load(open(os.path.join(G, fixture)))
+    assert ref["duration"] == 6 and ref["hidden"] == 1024
+    rows = {}
+    for s in sorted(int(k) for k in ref["runs"]):
+        r = ref["runs"][str(s)]
+        eng, snr, var = _fit6(dev, ref["steps"], s, ref["patience"], ref["lr0"])
+        losses, lrs = eng.history()
+        rl = np.array(r["loss"])
+        step_db = np.abs(10 * np.log10(losses / rl))
+        rows[s] = {"final_snr_gpu": snr, "final_snr_ref": r["snr_target"], "max_step_db": float(step_db.max()),
+                   "argmax_step": int(step_db.argmax()), "best_gpu": _db(var, np.min(losses)),
+                   "best_ref": _db(var, np.min(rl)), "drops_ref": int(np.sum(np.diff(r["lr"]) < 0))}
+        assert np.array_equal(lrs, np.array(r["lr"])), s
+    log(f"fit_5x1024_6s[{fixture}]", seeds=rows)
+    print("\n" + json.dumps(rows, indent=1))
+    if "_p3" in fixture:
+        assert all(v["drops_ref"] >= 1 for v in rows.values())
+    for s, v in rows.items():
+        assert abs(v["final_snr_gpu"] - v["final_snr_ref"]) < 0.1, (s, v)
+        assert abs(v["best_gpu"] - v["best_ref"]) < 0.1, (s, v)
+        assert v["max_step_db"] < STEP_DB, (s, v)
+
+
+# every step's loss of a 6 s run within this many dB of the reference's: measured worst step
+# 0.0011 dB over the three runs (final SNR within 0.0006 dB); the 0.1 dB SNR gates are north_star's
+STEP_DB = 0.01

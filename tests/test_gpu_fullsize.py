@@ -17,6 +17,10 @@ from errlog import log
 
 pytestmark = pytest.mark.gpu
 N = 1 << 20
+# the two splits differ only in fp32 summation order (split-K slabs, partial rows, the micro-batch
+# sum) and in the power-of-two dZ storage scale, which is exact above fp16's normal minimum:
+# measured 1.7e-7 overall, at most 1.6e-6 for one parameter (net.1.linear.weight)
+LINEARITY_TOL = 2e-5
 
 
 def _setup(dev, micro_batch=N, seed=0):
@@ -60,7 +64,12 @@ def test_fullsize_microbatch_linearity(dev):
     torch.cuda.synchronize()
     g1, g2 = one.grads.double(), two.grads.double()
     rel = float(torch.linalg.norm(g1 - g2) / torch.linalg.norm(g1))
-    assert rel < 1e-2, rel
+    lay = one.layout
+    per = {k: float(torch.linalg.norm(lay.view(g1, i) - lay.view(g2, i)) / torch.linalg.norm(lay.view(g1, i)))
+           for i, k in enumerate(lay.names)}
+    log("fullsize_microbatch_linearity", rel=rel, per_param=per)
+    assert rel < LINEARITY_TOL, (rel, per)
+    assert max(per.values()) < LINEARITY_TOL, per
     # the summed squared error rides the same vector: identical forward -> near-identical sum
     s1, s2 = float(g1[one.layout.sse_offset]), float(g2[two.layout.sse_offset])
     assert abs(s1 - s2) <= 1e-5 * s1

@@ -104,3 +104,28 @@ def test_snake_and_tanh_modules_vs_torch(dev, a0):
     vals = list(acts.values())
     assert len(vals) == 1 + 2 * 2 + 5        # input, 2 SineLayers x 2, Linear/Snake/Linear/Tanh/Linear
     assert rel(vals[-1].detach().cpu(), o.detach().cpu().double().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("a_shape", [(), (1,)])
+def test_snake_scalar_a_broadcasts(dev, a_shape):
+    """A scalar Snake `a` (the reference's formula broadcasts it over the columns, models.py:241)
+    is applied to every column and gets the column-summed gradient in its own shape; an `a` of
+    another length is refused instead of read out of bounds."""
+    from inr_for_audio_amd import _lib
+    from inr_for_audio_amd.models import fp32_act
+    torch.manual_seed(3)
+    x = torch.randn(700, 40, device=dev, requires_grad=True)
+    a = torch.full(a_shape, 0.7, device=dev, requires_grad=True)
+    y = fp32_act(x, _lib.FP32_SNAKE, a)
+    gy = torch.randn_like(y)
+    (y * gy).sum().backward()
+    xr = x.detach().clone().requires_grad_(True)
+    ar = a.detach().clone().requires_grad_(True)
+    yr = xr + (1.0 / ar) * torch.pow(torch.sin(xr * ar), 2)
+    (yr * gy).sum().backward()
+    assert a.grad.shape == a.shape
+    assert rel(y.detach().cpu(), yr.detach().cpu().double().numpy()) < 1e-5
+    assert rel(x.grad.cpu(), xr.grad.cpu().double().numpy()) < 1e-5
+    assert rel(a.grad.cpu().reshape(-1), ar.grad.cpu().double().numpy().reshape(-1)) < 1e-5
+    with pytest.raises(ValueError):
+        fp32_act(x, _lib.FP32_SNAKE, torch.ones(39, device=dev))
