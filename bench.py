@@ -54,6 +54,8 @@ KIND_MATCH = {  # profile kind -> (kernel-name substring, accepted template-argu
     "bwd_dx": ("gemm_nt_kernel", (", 1, false>", ", 1, false, true>")),
     "bwd_dx0": ("gemm_nt_kernel", (", 2, false>", ", 2, false, true>")),
     "bwd_dw": ("gemm_tn_kernel", ("",)),
+    # NT_FWD_HB: the last layer fused with the head, the loss gradient and the head backward
+    "head_fwd": ("gemm_nt_kernel", (", 7, true>",)),
 }
 
 
@@ -83,9 +85,10 @@ def pmc_traffic(kind: str):
 
 
 def pmc_mfma_util(kind: str):
-    """MFMA utilisation of `kind` at its actual clock from the newest committed
-    profiles/r*/bench_pmc_mfma.json (tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES over the SIMD
-    cycles implied by GRBM_GUI_ACTIVE), or None."""
+    """Ideal MFMA cycles of `kind` over (duration x clock) from the newest committed
+    profiles/r*/bench_pmc_mfma.json (tools/pmc_mfma.py), or None.  SQ_VALU_MFMA_BUSY_CYCLES is the
+    issued MFMA count x 16 on gfx950, so this restates the kernel time at the clock it ran at
+    (GRBM_GUI_ACTIVE); it is not an independent busy measurement."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "bench_pmc_mfma.json")))
     if not files or kind not in KIND_MATCH:
@@ -378,7 +381,7 @@ def main():
         eng.step()
     torch.cuda.synchronize(dev)
 
-    gemm_all = ("inner_fwd", "bwd_dx", "bwd_dw", "bwd_dx0")
+    gemm_all = ("inner_fwd", "head_fwd", "bwd_dx", "bwd_dw", "bwd_dx0")
     elapsed, prof, psteps, dom, (dom_ms, dom_n) = profiled_steps(
         eng, args, dev, dist, lib, _lib, 64 * (2 * L + 8) * eng.n_micro,
         lambda pr, n: max((k for k in gemm_all if pr[k][1]), key=lambda k: pr[k][0]))
@@ -425,7 +428,12 @@ def main():
                      "flops_per_launch": flops_gemm,
                      "hbm_gbs_at_traffic": (traffic / (kernels[dom]["avg_ms"] * 1e-3) / 1e9)
                      if traffic else None,
-                     "mfma_util_at_clock_pmc": pmc_mfma_util(dom) if headline else None},
+                     # = ideal MFMA cycles / (launch time x the clock it ran at): time x clock, not a
+                     # separate busy counter (pmc_mfma_util)
+                     "mfma_cycles_over_time_x_clock_pmc": pmc_mfma_util(dom) if headline else None},
+        # every GEMM kind's spec-peak fraction (the dominant one is `roofline`); head_fwd does the
+        # forward GEMM's flops plus the head, loss gradient and head backward
+        "gemm_frac_by_kind": {k: kernels[k]["tflops"] / PEAK_BF16_TFLOPS for k in gemm_kinds},
         "step_mfma_frac": inner_flops_step / (ms_per_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS,
         "gemm_mfma_frac": inner_flops_step / (gemm_ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS,
         "kernels": kernels,

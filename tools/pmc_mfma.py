@@ -8,6 +8,11 @@ cycles summed over the 8 XCDs.  So
 i.e. the fraction of the SIMDs' cycles at the clock the kernel actually ran at (the
 spec-peak fraction in bench.py's roofline also absorbs the clock drop below 2.4 GHz).
 
+What it is NOT: an independent busy measurement.  On gfx950 SQ_VALU_MFMA_BUSY_CYCLES equals the
+issued MFMA count x 16 (2^31 for every 2^20 x 1024 x 1024 GEMM in every profile), so mfma_util is
+ideal MFMA cycles / (duration x clock): the kernel time and the clock restated.  Its one use is
+the clock (GRBM_GUI_ACTIVE / duration) it folds in.
+
     python tools/pmc_mfma.py OUT.json DIR [kernel_trace.csv]
 """
 from __future__ import annotations
