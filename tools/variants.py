@@ -117,8 +117,19 @@ _HB_WAIT_OLD = """            while ((u = __hip_atomic_load(hpu + (size_t)jt * p
               __builtin_amdgcn_s_sleep(1);"""
 _HB_WAIT_NEW = """            u = __float_as_uint(own) + jt;"""
 
+# phase 2 without its dZ stores (the column partials still computed): WRONG dZ, timing only
+_HB_ST_OLD = """          st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));"""
+_HB_ST_NEW = """          if (gm[j] == 12345.0f) st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));"""
+# no phase 2 at all (only phase 1 and the hand-off): timing only
+_HB_PH2_OLD = """      for (int pp = 0; pp < SN / 2; ++pp) {
+        float cs[2][2][4];  // [db_L, dw_head][subtile h][column r]"""
+_HB_PH2_NEW = """      for (int pp = 0; pp < (p.n_valid == -7 ? SN / 2 : 0); ++pp) {
+        float cs[2][2][4];  // [db_L, dw_head][subtile h][column r]"""
+
 VARIANTS = {
     "hb_nowait": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW)]},
+    "hb_nostore": {"gemm_nt.hip": [(_HB_ST_OLD, _HB_ST_NEW)]},
+    "hb_noph2": {"gemm_nt.hip": [(_HB_PH2_OLD, _HB_PH2_NEW)]},
     "pkfma": {"gemm_nt.hip": [(_PK_OLD, _PK_NEW)]},
     "bst": {"gemm_nt.hip": [(_BST_OLD1, _BST_NEW1), (_BST_OLD2, _BST_NEW2)]},
     "st_sc1": {"gemm_nt.hip": [(_ST16, _st16_asm("sc1"))]},          # write-through epilogue stores
