@@ -11,7 +11,7 @@ summation order on the same seed moves it by as much -- DESIGN.md "Fit parity").
     own runs of the same seeds: the median over seeds of the best-loss SNR
     10 log10(var(target) / min_k loss_k) -- the error floor each run reaches, insensitive
     to where a spike happens to fall -- within north_star's 0.1 dB plus the fp32 reference's
-    own summation-order sensitivity on this fixture (a fixed 0.25 dB, BOUND_3X256).  The final SNR is a much
+    own summation-order sensitivity on this fixture (a fixed 0.35 dB, BOUND_3X256).  The final SNR is a much
     noisier statistic: bootstrapping the reference's 8 seeds gives its median a 5.5 dB
     standard deviation (7.8 dB for a difference of two such medians), so it is only checked
     one-sided at two standard deviations, GPU median >= reference median - 15 dB (a broken
@@ -19,10 +19,10 @@ summation order on the same seed moves it by as much -- DESIGN.md "Fit parity").
     steps, 4.0 dB bootstrap deviation) is checked at the same two deviations, +-11 dB.
 
 The headline model itself (SIREN 5x1024, omega0 = 3000) has its own fixture: the reference's
-run of 200 full-batch steps on gt_bach 1 s for 4 seeds (lr 1e-4 -- at run.py's 1e-3 this width
+run of 200 full-batch steps on gt_bach 1 s for 8 seeds (lr 1e-4 -- at run.py's 1e-3 this width
 does not leave the init plateau in 200 steps -- and patience 10, so ReduceLROnPlateau drops
-the lr inside the run).  The best-loss median within a fixed 2.1 dB (BOUND_5X1024_CHAOTIC: at lr
-1e-4 the fp32 reference itself moves 1.97 dB with its summation order), identical lr schedules
+the lr inside the run).  The best-loss median within a fixed 4.5 dB (BOUND_5X1024_CHAOTIC: at lr
+1e-4 the fp32 reference's own median moves 2.7 dB with its summation order), identical lr schedules
 while they track, and no fp16 overflow step.  North_star's 0.1 dB is held PER SEED in the stable
 regime (lr 3e-5) on gt_bach 1 s and on 6 s (264 600 coordinates, across a plateau lr drop).
 """
@@ -77,14 +77,15 @@ def _torch_gpu_best(dev, var, seed, steps, H=256, L=2, w0=1000.0, lr=1e-3, patie
 
 
 # Fixed bounds on |median over seeds of the GPU's best-loss SNR - the reference's| (dB) for the two
-# chaotic multi-seed fixtures: north_star's 0.1 dB plus the fp32 reference algorithm's own
-# sensitivity to summation order on that fixture, measured ONCE as |median(torch fp32 eager on the
-# GPU) - median(CPU reference)| over the fixture's seeds (r11: 0.15 dB for 3x256 over 8 seeds;
-# 1.97 dB for the 5x1024 lr 1e-4 run over 4 seeds).  The torch fp32 runs are still made and
-# logged, but no longer widen the gate.  The per-seed 0.1 dB gates are the stable-regime tests
-# (1 s and 6 s) at the end of this file.
-BOUND_3X256 = 0.25
-BOUND_5X1024_CHAOTIC = 2.1
+# chaotic multi-seed fixtures: north_star's 0.1 dB plus two standard deviations of how far the
+# reference algorithm's OWN median moves when only its summation order changes -- a paired
+# bootstrap (20 000 resamples of the seeds) of median(torch fp32 eager on the GPU) - median(CPU
+# reference), measured once over the fixture's 8 seeds (round 3: 3x256 +0.15 dB, std 0.11 dB;
+# 5x1024 at lr 1e-4 -2.66 dB, std 2.2 dB, the per-seed shifts reaching 10.6 dB).  The torch fp32
+# runs are still made and logged, but no longer widen the gate.  The per-seed 0.1 dB gates are the
+# stable-regime tests (1 s and 6 s) at the end of this file.
+BOUND_3X256 = 0.35
+BOUND_5X1024_CHAOTIC = 4.5
 
 
 def test_fit_first_steps_track_reference(dev):
