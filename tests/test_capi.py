@@ -74,6 +74,17 @@ def test_validation_without_device(lib):
     assert lib.siren_first_fwd(1, 3, 1, 1, ctypes.c_float(1.0), 128, 256, 1, 1, None) == 1003
     assert lib.siren_coords_fill_grid(None, 8, 0, 4, 2, None) == 1002
     assert lib.siren_coords_fill_grid(1, 8, 0, 0, 2, None) == 1001        # height 0
+    # the fused head: NULL operands, rows not a multiple of 256, a loss mode other than MSE / L1
+    f = ctypes.c_float
+    assert lib.siren_head_fused_fwd(None, 1, 1, f(30), 1024, 256, 1, 1, f(0), 1, 1024, 1024.0, 0, 1, 1, 1, 1, 1, 1,
+                                    1, 1, None) == 1002
+    assert lib.siren_head_fused_fwd(1, 1, 1, f(30), 1152, 256, 1, 1, f(0), 1, 1152, 1152.0, 0, 1, 1, 1, 1, 1, 1,
+                                    1, 1, None) == 1001
+    assert lib.siren_head_fused_fwd(1, 1, 1, f(30), 1024, 256, 1, 1, f(0), 1, 1024, 1024.0, 2, 1, 1, 1, 1, 1, 1,
+                                    1, 1, None) == 1003
+    assert lib.siren_grad_scale_bound(None, 10, None, 1, 1, 256, 10.0, f(0), 0, f(30), 1, None) == 1002
+    assert lib.siren_grad_scale_bound(1, -1, 1, 1, 1, 256, 10.0, f(0), 0, f(30), 1, None) == 1001
+    assert lib.siren_grad_scale_bound(1, 10, 1, 1, 1, 256, 10.0, f(0), 3, f(30), 1, None) == 1003
     b = SirenBatch()
     b.loss_mode = 7                                                          # not MSE / L1
     net.hidden = 256

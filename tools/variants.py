@@ -126,7 +126,15 @@ _HB_PH2_OLD = """      for (int pp = 0; pp < SN / 2; ++pp) {
 _HB_PH2_NEW = """      for (int pp = 0; pp < (p.n_valid == -7 ? SN / 2 : 0); ++pp) {
         float cs[2][2][4];  // [db_L, dw_head][subtile h][column r]"""
 
+# forward stores folded onto the first 512 rows of Y / C (1 MB each: L2-resident, no HBM write-back):
+# WRONG outputs, timing only -- prices the forward's 4.3 GB of output writes against HBM
+_L2ST_OLD = """          st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
+          st16(p.C + rowoff + npc + pp * 32, cpk[pp]);"""
+_L2ST_NEW = """          st16(p.Y + (rowoff & (size_t)(512 * N - 1)) + npc + pp * 32, yp[pp]);
+          st16(p.C + (rowoff & (size_t)(512 * N - 1)) + npc + pp * 32, cpk[pp]);"""
+
 VARIANTS = {
+    "st_l2": {"gemm_nt.hip": [(_L2ST_OLD, _L2ST_NEW)]},
     "hb_nowait": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW)]},
     "hb_nostore": {"gemm_nt.hip": [(_HB_ST_OLD, _HB_ST_NEW)]},
     "hb_noph2": {"gemm_nt.hip": [(_HB_PH2_OLD, _HB_PH2_NEW)]},
