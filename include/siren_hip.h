@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 9
+#define SIREN_ABI_VERSION 10
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 /* ints in one tile-queue counter set (siren_batch.tileq, siren_inner_fwd's tileq): the
@@ -139,7 +139,7 @@ typedef struct siren_batch {
   float* gscale;         /* [2]  {S, 1/S} of this micro-batch's backward        */
   float* col_part;       /* [rows/128][max(2, 2+in)][H]                         */
   float* col_part2;      /* [rows/128][H]                                       */
-  float* red_tmp;        /* [64][H]                                             */
+  float* red_tmp;        /* [4][64][H]  (ABI 10; was [64][H])                   */
   float* slab;           /* [splits][H][H]                                      */
   uint16_t* E[SIREN_MAX_INNER + 1];  /* E[i+1] fp16 [rows][H]: dY/da of Snake inner layer
                                         i; E[0]: of a Linear + Snake first layer (NULL

@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 MAX_INNER = 16
 ROW_TILE = 128
 TILEQ_INTS = 768  # SIREN_TILEQ_INTS: one tile-queue counter set

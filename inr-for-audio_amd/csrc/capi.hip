@@ -10,6 +10,7 @@ using namespace siren;
 static_assert(sizeof(siren_opt_state) == sizeof(OptState), "opt state layout");
 static_assert(sizeof(siren_guard) == sizeof(GuardState), "guard layout");
 static_assert(SIREN_TILEQ_INTS == kTileqInts, "tile-queue set size");
+static_assert(SIREN_MAX_INNER == siren::kMaxInner, "max hidden layers");
 static_assert((int)SIREN_FP32_SNAKE == (int)siren::FP32_SNAKE && (int)SIREN_FP32_SIN == (int)siren::FP32_SIN &&
                   (int)SIREN_FP32_TANH == (int)siren::FP32_TANH, "fp32 act codes");
 
@@ -32,6 +33,7 @@ struct ProfState {
   uint32_t mask = 0xffffffffu;  // kinds bracketed (siren_profile_mask)
   std::vector<hipEvent_t> ev;   // 2 per record
   std::vector<int> kind;
+  std::vector<int> nl;          // launches inside each record
   int used = 0;
 };
 ProfState g_prof;
@@ -43,9 +45,10 @@ inline void prof_begin(int kind, hipStream_t s) {
   g_prof.kind[g_prof.used] = kind;
   g_prof.open = true;
 }
-inline void prof_end(hipStream_t s) {
+inline void prof_end(hipStream_t s, int launches = 1) {
   if (!g_prof.open) return;
   (void)hipEventRecord(g_prof.ev[2 * g_prof.used + 1], s);
+  g_prof.nl[g_prof.used] = launches;
   g_prof.used++;
   g_prof.open = false;
 }
@@ -110,6 +113,14 @@ inline hipError_t mark_ready(const siren_batch* b, int k, hipStream_t s) {
   return b->grad_ready[k] ? hipEventRecord((hipEvent_t)b->grad_ready[k], s) : hipSuccess;
 }
 
+// one segment of a multi-segment column reduction (capi's sets never exceed kMaxColSegs)
+inline void seg_add(ColSegs& sg, const float* src, float* out, int out_stride = 1) {
+  sg.src[sg.n] = src;
+  sg.out[sg.n] = out;
+  sg.out_stride[sg.n] = out_stride;
+  ++sg.n;
+}
+
 // SIREN_OPT_HEAD_FUSE: siren_train_step runs the last layer as NT_FWD_HB when it can
 int g_head_fuse = 1;
 bool head_fused(const siren_net* n, const siren_batch* b) {
@@ -123,6 +134,14 @@ hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s, bool h
   SIREN_PROF(SIREN_PROF_FIRST_FWD, s, first_fwd(b->coords, n->in_dim, n->W0, n->b0, n->omega0, R, H, B(b->Y[0]),
                                                 B(b->C[0]), s, n->first_snake ? n->a0 : nullptr,
                                                 n->first_snake ? B(b->E[0]) : nullptr));
+  // the run of plain forward layers is ONE profiling record (back-to-back launches: one event
+  // pair per run instead of per launch, so the per-launch dispatch latency inside the bracket
+  // is paid once; bench.py divides by the launch count)
+  int run = 0;
+  auto close_run = [&]() {
+    if (run > 0) prof_end(s, run);
+    run = 0;
+  };
   for (int i = 0; i < L; ++i) {
     NtParams p = {};
     p.X = B(b->Y[i]);
@@ -144,11 +163,19 @@ hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s, bool h
       p.sse_part = b->sse_part; p.gsum_part = b->gsum_part;
       p.n_valid = b->n_valid; p.loss_mode = b->loss_mode; p.gfac = gfac; p.head_omega = n->head_omega;
       p.gscale = b->gscale; p.dZ = B(b->dZ[0]); p.colsum_part = b->col_part;
+      close_run();
       SIREN_PROF(SIREN_PROF_HEAD_FWD, s, gemm_nt(NT_FWD_HB, true, p, s));
       continue;
     }
-    SIREN_PROF(SIREN_PROF_INNER_FWD, s, gemm_nt(fwd_mode(n->act[i]), head, p, s));
+    if (run == 0) prof_begin(SIREN_PROF_INNER_FWD, s);
+    const hipError_t e = gemm_nt(fwd_mode(n->act[i]), head, p, s);
+    if (e != hipSuccess) {
+      close_run();
+      return e;
+    }
+    if (g_prof.open) ++run;
   }
+  close_run();
   return hipSuccess;
 }
 
@@ -236,8 +263,10 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
   const int ntile = nt_choose_tile(R, H), tntile = tn_choose_tile(R, H, H);
   const int prow = R / ntile;  // partial rows written by the NT_DX / NT_DX0 epilogues
   if (hb) {
-    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + H, 2 * H, prow, H, gr->w_head, 1, 1, b->red_tmp, s));
-    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, 2 * H, prow, H, gr->b[L - 1], 1, 1, b->red_tmp, s));
+    ColSegs sg = {};
+    seg_add(sg, b->col_part + H, gr->w_head);
+    seg_add(sg, b->col_part, gr->b[L - 1]);
+    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce_multi(sg, 2 * H, prow, H, 1, b->red_tmp, s));
   } else {
     const bool snake_last = net->act[L - 1] == SIREN_ACT_SNAKE;
     float* da_last = b->col_part + (int64_t)(R / 128) * H;  // second H-wide slab of col_part
@@ -247,10 +276,11 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
     SIREN_PROF(SIREN_PROF_HEAD, s, head_bwd(B(b->C[L]), B(b->Y[L]), b->g, net->w_head, act_omega(net, L - 1),
                                             R, H, b->gscale, B(b->dZ[0]), b->col_part, b->col_part2,
                                             snake_last ? B(b->E[L]) : nullptr, snake_last ? da_last : nullptr, s));
-    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part2, H, R / 128, H, gr->w_head, 1, 1, b->red_tmp, s));
-    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, H, R / 128, H, gr->b[L - 1], 1, 1, b->red_tmp, s));
-    if (snake_last)
-      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(da_last, H, R / 128, H, gr->a[L - 1], 1, 1, b->red_tmp, s));
+    ColSegs sg = {};
+    seg_add(sg, b->col_part2, gr->w_head);
+    seg_add(sg, b->col_part, gr->b[L - 1]);
+    if (snake_last) seg_add(sg, da_last, gr->a[L - 1]);
+    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce_multi(sg, H, R / 128, H, 1, b->red_tmp, s));
   }
   SIREN_TRY(mark_ready(b, L + 1, s));  // head: w_head, b_head (and sse, summed before the backward)
 
@@ -284,10 +314,10 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
       p.dZ = B(b->dZ[cur ^ 1]);
       SIREN_PROF(SIREN_PROF_BWD_DX, s, gemm_nt(snake ? NT_DX_SNAKE : NT_DX, false, p, s));
       const int64_t rs = (int64_t)(snake ? 2 : 1) * H;
-      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, rs, prow, H, gr->b[i - 1], 1, 1, b->red_tmp, s));
-      if (snake)
-        SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + H, rs, prow, H, gr->a[i - 1], 1, 1,
-                                                    b->red_tmp, s));
+      ColSegs sg = {};
+      seg_add(sg, b->col_part, gr->b[i - 1]);
+      if (snake) seg_add(sg, b->col_part + H, gr->a[i - 1]);
+      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce_multi(sg, rs, prow, H, 1, b->red_tmp, s));
       cur ^= 1;
     } else {
       const bool fs = net->first_snake != 0;
@@ -298,13 +328,12 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
       p.in_dim = in;
       SIREN_PROF(SIREN_PROF_BWD_DX0, s, gemm_nt(fs ? NT_DX0_SNAKE : NT_DX0, false, p, s));
       const int64_t rs = (int64_t)(fs ? 2 + in : 1 + in) * H;
-      if (fs)
-        SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + (int64_t)(1 + in) * H, rs, prow, H, gr->a0, 1, 1,
-                                                    b->red_tmp, s));
-      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part, rs, prow, H, gr->b0, 1, 1, b->red_tmp, s));
-      for (int j = 0; j < in; ++j)
-        SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce(b->col_part + (int64_t)(1 + j) * H, rs, prow, H,
-                                                    gr->W0 + j, in, 1, b->red_tmp, s));
+      // db0, the in columns of dW0 (stride in) and a0: one launch pair
+      ColSegs sg = {};
+      if (fs) seg_add(sg, b->col_part + (int64_t)(1 + in) * H, gr->a0);
+      seg_add(sg, b->col_part, gr->b0);
+      for (int j = 0; j < in; ++j) seg_add(sg, b->col_part + (int64_t)(1 + j) * H, gr->W0 + j, in);
+      SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce_multi(sg, rs, prow, H, 1, b->red_tmp, s));
       SIREN_TRY(mark_ready(b, L, s));
     }
   }
@@ -341,8 +370,7 @@ int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b
                                              b->target, b->n_valid, gfac, b->out, b->g, b->sse_part,
                                              b->gsum_part, b->gmax_part, s, net->head_omega, b->loss_mode));
   const int nsum = (R + 255) / 256;
-  SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->sse_part, nsum, gr->sse, 1, s));
-  SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to(b->gsum_part, nsum, gr->b_head, 1, s));
+  SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to2(b->sse_part, gr->sse, b->gsum_part, gr->b_head, nsum, 1, s));
   // ---- backward (autograd of run.py:185) ----
   return run_backward(net, gr, b, s, hb);
 }
@@ -374,12 +402,20 @@ int siren_apply_update(const siren_net* net, float* params, const float* grads_f
   if (!params || !grads_flat || !exp_avg || !exp_avg_sq || !state || !sse || !W_fp32 || !Wh || !WTh)
     return SIREN_ERR_NULL;
   hipStream_t s = S(stream);
+  // the fp16 shadows of every hidden layer, refreshed by one launch after Adam
+  CastSet cs = {};
+  cs.n = net->n_inner;
+  for (int i = 0; i < net->n_inner; ++i) {
+    if (!W_fp32[i] || !Wh[i] || !WTh[i]) return SIREN_ERR_NULL;
+    cs.W[i] = W_fp32[i];
+    cs.Wb[i] = B(Wh[i]);
+    cs.WTb[i] = B(WTh[i]);
+  }
   GuardState* gd = (GuardState*)guard;
   if (gd) SIREN_PROF(SIREN_PROF_UPDATE, s, guard_check(grads_flat, n_params, gd, s));
   SIREN_PROF(SIREN_PROF_UPDATE, s, adam_flat(params, grads_flat, exp_avg, exp_avg_sq, n_params,
                                              (const OptState*)state, s, gd, sse));
-  for (int i = 0; i < net->n_inner; ++i)
-    SIREN_PROF(SIREN_PROF_UPDATE, s, cast_weight(W_fp32[i], net->hidden, net->hidden, B(Wh[i]), B(WTh[i]), s));
+  SIREN_PROF(SIREN_PROF_UPDATE, s, cast_weights(cs, net->hidden, s));
   SIREN_PROF(SIREN_PROF_UPDATE, s, plateau_step((OptState*)state, sse, n_total, loss_hist, lr_hist, hist_cap, s,
                                                 gd));
   return SIREN_OK;
@@ -670,12 +706,14 @@ int siren_profile_enable(int32_t max_records) {
   for (hipEvent_t e : g_prof.ev) (void)hipEventDestroy(e);
   g_prof.ev.clear();
   g_prof.kind.clear();
+  g_prof.nl.clear();
   g_prof.used = 0;
   g_prof.on = false;
   if (max_records <= 0) return SIREN_OK;
   g_prof.ev.resize(2 * (size_t)max_records);
   for (auto& e : g_prof.ev) SIREN_TRY(hipEventCreate(&e));
   g_prof.kind.assign(max_records, -1);
+  g_prof.nl.assign(max_records, 1);
   g_prof.on = true;
   return SIREN_OK;
 }
@@ -700,7 +738,7 @@ int siren_profile_read(int32_t kind, double* total_ms, int64_t* count) {
     float ms = 0.f;
     SIREN_TRY(hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]));
     tot += ms;
-    ++n;
+    n += g_prof.nl[i];
   }
   *total_ms = tot;
   *count = n;

@@ -413,10 +413,13 @@ hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_h
 
 // ---------------------------------------------------------------------------------
 // Deterministic column reduction of partial rows, two passes of the same kernel:
-// pass 1 sums row chunks into tmp[64][ncols], pass 2 sums those 64 rows.
-__global__ void col_reduce_kernel(const float* __restrict__ part, int64_t row_stride, int nrows,
-                                  int ncols, float* __restrict__ out, int64_t out_row_stride,
-                                  int out_stride, int accumulate) {
+// pass 1 sums row chunks into tmp[64][ncols], pass 2 sums those 64 rows.  Up to kMaxColSegs
+// reductions of one partial-row layout (same row stride and row count, e.g. db and the dW0
+// columns of one NT_DX0 epilogue) share the two launches: segment z = blockIdx.z, with its own
+// 64-row slice of tmp; every segment's summation order is the one-segment order.
+__device__ __forceinline__ void col_reduce_block(const float* __restrict__ part, int64_t row_stride, int nrows,
+                                                 int ncols, float* __restrict__ out, int64_t out_row_stride,
+                                                 int out_stride, int accumulate) {
   __shared__ float red[4][64];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rg = threadIdx.x >> 6;
@@ -435,20 +438,43 @@ __global__ void col_reduce_kernel(const float* __restrict__ part, int64_t row_st
   }
 }
 
-hipError_t col_reduce(const float* part, int64_t row_stride, int nrows, int ncols, float* out,
-                      int out_stride, int accumulate, float* tmp, hipStream_t s) {
+// pass: 0 = one pass (part -> out), 1 = row chunks -> tmp, 2 = tmp -> out
+__global__ void col_reduce_kernel(ColSegs sg, int64_t row_stride, int nrows, int ncols, int pass, float* tmp,
+                                  int accumulate) {
+  const int z = blockIdx.z;
+  float* tz = tmp + (int64_t)z * 64 * ncols;
+  if (pass == 0)
+    col_reduce_block(sg.src[z], row_stride, nrows, ncols, sg.out[z], 0, sg.out_stride[z], accumulate);
+  else if (pass == 1)
+    col_reduce_block(sg.src[z], row_stride, nrows, ncols, tz, ncols, 1, 0);
+  else
+    col_reduce_block(tz, ncols, 64, ncols, sg.out[z], 0, sg.out_stride[z], accumulate);
+}
+
+hipError_t col_reduce_multi(const ColSegs& sg, int64_t row_stride, int nrows, int ncols, int accumulate, float* tmp,
+                            hipStream_t s) {
+  if (sg.n < 1 || sg.n > kMaxColSegs) return hipErrorInvalidValue;
   const int cb = (ncols + 63) / 64;
   if (nrows <= 256) {
-    hipLaunchKernelGGL(col_reduce_kernel, dim3(cb, 1), dim3(256), 0, s, part, row_stride, nrows, ncols,
-                       out, (int64_t)0, out_stride, accumulate);
+    hipLaunchKernelGGL(col_reduce_kernel, dim3(cb, 1, sg.n), dim3(256), 0, s, sg, row_stride, nrows, ncols, 0,
+                       tmp, accumulate);
     return hipGetLastError();
   }
-  const int chunks = 64;
-  hipLaunchKernelGGL(col_reduce_kernel, dim3(cb, chunks), dim3(256), 0, s, part, row_stride, nrows,
-                     ncols, tmp, (int64_t)ncols, 1, 0);
-  hipLaunchKernelGGL(col_reduce_kernel, dim3(cb, 1), dim3(256), 0, s, (const float*)tmp, (int64_t)ncols,
-                     chunks, ncols, out, (int64_t)0, out_stride, accumulate);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3(cb, 64, sg.n), dim3(256), 0, s, sg, row_stride, nrows, ncols, 1, tmp,
+                     0);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3(cb, 1, sg.n), dim3(256), 0, s, sg, row_stride, nrows, ncols, 2, tmp,
+                     accumulate);
   return hipGetLastError();
+}
+
+hipError_t col_reduce(const float* part, int64_t row_stride, int nrows, int ncols, float* out,
+                      int out_stride, int accumulate, float* tmp, hipStream_t s) {
+  ColSegs sg = {};
+  sg.n = 1;
+  sg.src[0] = part;
+  sg.out[0] = out;
+  sg.out_stride[0] = out_stride;
+  return col_reduce_multi(sg, row_stride, nrows, ncols, accumulate, tmp, s);
 }
 
 // out[0] (+)= sum(x[0..n))  -- single block, fixed order.
@@ -462,6 +488,23 @@ __global__ void sum_to_kernel(const float* __restrict__ x, int n, float* out, in
 
 hipError_t sum_to(const float* x, int n, float* out, int accumulate, hipStream_t s) {
   hipLaunchKernelGGL(sum_to_kernel, dim3(1), dim3(1024), 0, s, x, n, out, accumulate);
+  return hipGetLastError();
+}
+
+// two independent sum_to in one launch (block z: x_z -> out_z), each in sum_to's order
+__global__ void sum_to2_kernel(const float* __restrict__ x0, float* out0, const float* __restrict__ x1, float* out1,
+                               int n, int accumulate) {
+  __shared__ float scratch[16];
+  const float* x = blockIdx.x ? x1 : x0;
+  float* out = blockIdx.x ? out1 : out0;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[i];
+  s = block_sum(s, scratch);
+  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + s : s;
+}
+
+hipError_t sum_to2(const float* x0, float* out0, const float* x1, float* out1, int n, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(sum_to2_kernel, dim3(2), dim3(1024), 0, s, x0, out0, x1, out1, n, accumulate);
   return hipGetLastError();
 }
 
@@ -603,6 +646,30 @@ hipError_t cast_weight(const float* W, int H_out, int H_in, h16* Wb, h16* WTb, h
   if (H_out % 64 || H_in % 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(cast_weight_kernel, dim3(H_in / 64, H_out / 64), dim3(256), 0, s, W, H_out, H_in,
                      Wb, WTb);
+  return hipGetLastError();
+}
+
+// the shadows of every hidden layer (square H x H) in one launch: layer = blockIdx.z
+__global__ void cast_weights_kernel(CastSet cs, int H) {
+  const int l = blockIdx.z;
+  __shared__ float tile[64][65];
+  const float* __restrict__ W = cs.W[l];
+  h16* __restrict__ Wb = cs.Wb[l];
+  h16* __restrict__ WTb = cs.WTb[l];
+  const int o0 = blockIdx.y * 64, k0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const float w = W[(size_t)(o0 + r) * H + k0 + tx];
+    tile[r][tx] = w;
+    Wb[(size_t)(o0 + r) * H + k0 + tx] = (h16)w;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) WTb[(size_t)(k0 + r) * H + o0 + tx] = (h16)tile[tx][r];
+}
+
+hipError_t cast_weights(const CastSet& cs, int H, hipStream_t s) {
+  if (H % 64 || cs.n < 1 || cs.n > kMaxInner) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cast_weights_kernel, dim3(H / 64, H / 64, cs.n), dim3(256), 0, s, cs, H);
   return hipGetLastError();
 }
 

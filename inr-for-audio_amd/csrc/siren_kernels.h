@@ -132,6 +132,17 @@ hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_h
 // out[c*out_stride] (+)= sum_r part[r*row_stride + c]; tmp holds >= 64*ncols floats
 hipError_t col_reduce(const float* part, int64_t row_stride, int nrows, int ncols, float* out,
                       int out_stride, int accumulate, float* tmp, hipStream_t s);
+// up to kMaxColSegs col_reduce of one partial-row layout in one launch pair (results identical to
+// one col_reduce per segment); tmp holds >= n*64*ncols floats
+constexpr int kMaxColSegs = 4;
+struct ColSegs {
+  const float* src[kMaxColSegs];
+  float* out[kMaxColSegs];
+  int out_stride[kMaxColSegs];
+  int n;
+};
+hipError_t col_reduce_multi(const ColSegs& sg, int64_t row_stride, int nrows, int ncols, int accumulate, float* tmp,
+                            hipStream_t s);
 
 // unfused fp32 layers (layer_fp32.hip): lone SineLayer / Linear / Snake / Tanh modules
 enum Fp32Act { FP32_IDENTITY = 0, FP32_SIN = 1, FP32_TANH = 2, FP32_SNAKE = 3 };  // == siren_fp32_act
@@ -187,6 +198,17 @@ hipError_t adam_flat(float* p, const float* g, float* m, float* v, int64_t n, co
 hipError_t plateau_step(OptState* st, const float* sse, double n_total, float* loss_hist,
                         double* lr_hist, int64_t hist_cap, hipStream_t s, GuardState* guard = nullptr);
 hipError_t cast_weight(const float* W, int H_out, int H_in, h16* Wb, h16* WTb, hipStream_t s);
+// cast_weight of n square H x H layers in one launch
+constexpr int kMaxInner = 16;  // == SIREN_MAX_INNER
+struct CastSet {
+  const float* W[kMaxInner];
+  h16* Wb[kMaxInner];
+  h16* WTb[kMaxInner];
+  int n;
+};
+hipError_t cast_weights(const CastSet& cs, int H, hipStream_t s);
 hipError_t sum_to(const float* x, int n, float* out, int accumulate, hipStream_t s);
+// sum_to(x0 -> out0) and sum_to(x1 -> out1) in one launch
+hipError_t sum_to2(const float* x0, float* out0, const float* x1, float* out1, int n, int accumulate, hipStream_t s);
 
 }  // namespace siren

@@ -129,7 +129,7 @@ class Workspace:
             self.dZ = [e(R, H, dtype=h) for _ in range(2)]
             self.col_part = e(R // 128, max(2 + spec.in_dim, 2), H)
             self.col_part2 = e(R // 128, H)
-            self.red_tmp = e(64, H)
+            self.red_tmp = e(4, 64, H)  # ABI 10: up to 4 column reductions per launch pair
             self.slab = e(int(lib.siren_slab_floats(H, self.splits)))
         else:
             self.splits = 1

@@ -44,7 +44,7 @@ def test_struct_layouts_match(lib):
 
 
 def test_host_only_helpers(lib):
-    assert lib.siren_abi_version() == 9
+    assert lib.siren_abi_version() == 10
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256

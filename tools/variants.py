@@ -133,7 +133,54 @@ _L2ST_OLD = """          st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
 _L2ST_NEW = """          st16(p.Y + (rowoff & (size_t)(512 * N - 1)) + npc + pp * 32, yp[pp]);
           st16(p.C + (rowoff & (size_t)(512 * N - 1)) + npc + pp * 32, cpk[pp]);"""
 
+# forward epilogue computes everything but issues no stores (a never-true guard keeps the values):
+# WRONG outputs, timing only -- the epilogue's VALU alone against its stores
+_NOST_NEW = """          if (yp[pp].x == 0x12345u && cpk[pp].y == 0x6789u) {
+            st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
+            st16(p.C + rowoff + npc + pp * 32, cpk[pp]);
+          }"""
+
+# whole 128-B line dZ stores in the NT_DX epilogue (both 16-B pieces of a row subtile computed
+# first, then traded as in "fl")
+_DXFL_OLD1 = """#pragma unroll
+        for (int pp = 0; pp < SN / 2; ++pp) {
+          uint2 cpu[2];"""
+_DXFL_NEW1 = """        uint4 dzq[SN / 2];
+#pragma unroll
+        for (int pp = 0; pp < SN / 2; ++pp) {
+          uint2 cpu[2];"""
+_DXFL_OLD2 = """          if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE)
+            st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+        }"""
+_DXFL_NEW2 = """          if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
+        }
+        if constexpr (MODE == NT_DX && SN == 4) {
+          const bool hi = (lane & 8) != 0;
+          const size_t ra = (size_t)(m0 + wm * TM + j * 16 + (lane & 7)) * N + npc + (hi ? 32 : 0);
+          const uint4 send = hi ? dzq[0] : dzq[1];
+          uint4 recv;
+          recv.x = __builtin_amdgcn_update_dpp(0, (int)send.x, 0x128, 0xf, 0xf, false);
+          recv.y = __builtin_amdgcn_update_dpp(0, (int)send.y, 0x128, 0xf, 0xf, false);
+          recv.z = __builtin_amdgcn_update_dpp(0, (int)send.z, 0x128, 0xf, 0xf, false);
+          recv.w = __builtin_amdgcn_update_dpp(0, (int)send.w, 0x128, 0xf, 0xf, false);
+          st16(p.dZ + ra, hi ? recv : dzq[0]);
+          st16(p.dZ + ra + (size_t)8 * N, hi ? dzq[1] : recv);
+        } else if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE) {
+#pragma unroll
+          for (int pp = 0; pp < SN / 2; ++pp) st16(p.dZ + rowoff + npc + pp * 32, dzq[pp]);
+        }"""
+
+# dW GEMM operands from 8 K-steps of the slice only (L2-resident Y and dZ): WRONG dW, timing only --
+# prices the dW K-loop's operand latency
+_DWL2_OLD = """        const int ks = ks_begin + min(kt, nkl - 1);  // past the slice: a consumed piece re-read"""
+_DWL2_NEW = """        const int ks = ks_begin + (min(kt, nkl - 1) & 7);"""
+
 VARIANTS = {
+    "dw_l2": {"gemm_tn.hip": [(_DWL2_OLD, _DWL2_NEW)]},
+    "dxfl": {"gemm_nt.hip": [(_DXFL_OLD1, _DXFL_NEW1), (_DXFL_OLD2, _DXFL_NEW2)]},
+    "fl_dxfl": {"gemm_nt.hip": [(_FL_OLD, _FL_NEW), (_DXFL_OLD1, _DXFL_NEW1), (_DXFL_OLD2, _DXFL_NEW2)]},
+    "st_none": {"gemm_nt.hip": [(_L2ST_OLD, _NOST_NEW)]},
+    "fl_nt": {"gemm_nt.hip": [(_ST16, _st16_asm("nt")), (_FL_OLD, _FL_NEW)]},  # whole-line non-temporal
     "st_l2": {"gemm_nt.hip": [(_L2ST_OLD, _L2ST_NEW)]},
     "hb_nowait": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW)]},
     "hb_nostore": {"gemm_nt.hip": [(_HB_ST_OLD, _HB_ST_NEW)]},
