@@ -37,6 +37,14 @@
 #include "siren_common.h"
 #include "siren_kernels.h"
 
+// rows per Cprev/Eprev batch in the Snake dX epilogues (gemm_nt_kernel): NT_DX_SNAKE, NT_DX0_SNAKE
+#ifndef SIREN_SNAKE_EB
+#define SIREN_SNAKE_EB 4
+#endif
+#ifndef SIREN_SNAKE0_EB
+#define SIREN_SNAKE0_EB 8
+#endif
+
 #ifdef SIREN_DIAG
 #define SIREN_DIAG_ON 1
 #else
@@ -90,8 +98,10 @@ struct NtLds {
   static constexpr int BIAS = Cfg::RING + Cfg::RED;
   static constexpr int HW = BIAS + (nt_is_fwd(MODE) ? Cfg::VEC : 0);
   static constexpr int A = HW + (HEAD ? Cfg::VEC : 0);
-  static constexpr int QS = A + (MODE == NT_FWD_SNAKE ? Cfg::VEC : 0);  // dynamic tile queue: 2 tile ids
+  static constexpr int IA = A + (MODE == NT_FWD_SNAKE ? Cfg::VEC : 0);   // Snake 1/a, divided once
+  static constexpr int QS = IA + (MODE == NT_FWD_SNAKE ? Cfg::VEC : 0);  // dynamic tile queue: 2 tile ids
   static constexpr int SIZE = QS + 16;
+  static_assert(SIZE <= 160 * 1024, "LDS");
 };
 
 // Tile-queue counter set (caller-owned, SIREN_TILEQ_INTS ints): 8 shard heads 128 B apart, then
@@ -228,20 +238,38 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
   float* bias_lds = (float*)(smem + Lay::BIAS);
   float* hw_lds = (float*)(smem + Lay::HW);
-  float* a_lds = (float*)(smem + Lay::A);  // Snake: a
+  float* a_lds = (float*)(smem + Lay::A);    // Snake: a
+  float* ia_lds = (float*)(smem + Lay::IA);  // Snake: 1/a (the same IEEE quotient the epilogue used per element)
   if constexpr (nt_is_fwd(MODE)) {
     for (int c = tid * 4; c < N; c += Cfg::THREADS * 4) {
       *(float4*)(bias_lds + c) = *(const float4*)(p.bias + c);
       if constexpr (HEAD) *(float4*)(hw_lds + c) = *(const float4*)(p.head_w + c);
-      if constexpr (MODE == NT_FWD_SNAKE) *(float4*)(a_lds + c) = *(const float4*)(p.act_a + c);
+      if constexpr (MODE == NT_FWD_SNAKE) {
+        const float4 a4 = *(const float4*)(p.act_a + c);
+        *(float4*)(a_lds + c) = a4;
+        *(float4*)(ia_lds + c) = float4{1.0f / a4.x, 1.0f / a4.y, 1.0f / a4.z, 1.0f / a4.w};
+      }
     }
     // visible to other waves after the pipeline's first barrier
   }
   // dZ carries the backward storage scale S; the fp32 column partials leave unscaled
   const float inv_scale = (!nt_is_fwd(MODE) && p.gscale) ? p.gscale[1] : 1.0f;
-  // NT_DX / NT_DX0 epilogue operands loaded by `pre` (before the next tile's early prefetch)
-  constexpr int PRE_J = nt_is_fwd(MODE) ? 0 : (MODE == NT_DX ? SM : SM / 2);
+  // NT_DX / NT_DX0 epilogue operands loaded by `pre` (before the next tile's early prefetch).  The
+  // rest are loaded by the epilogue in one batch once earlier pieces are consumed (their
+  // accumulators free the registers), so a batch waits once, not once per piece behind the
+  // in-order vmcnt (which also covers the next tile's stages and this tile's stores).  NT_DX
+  // preloads every row; NT_DX0 rows 0 .. SM/2-1.  The Snake modes (Cprev AND Eprev per piece) go
+  // column pair by column pair: `pre` loads pair 0 of every row, the epilogue pair 1 after pair 0.
+  constexpr bool HAS_E = (MODE == NT_DX_SNAKE || MODE == NT_DX0_SNAKE);
+  constexpr int PRE_J = (nt_is_fwd(MODE) || HAS_E) ? 0 : (MODE == NT_DX ? SM : SM / 2);
+  // Snake modes: batches of EB rows of one column pair (pair 0 rows 0 .. EB-1 from `pre`)
+  // (fewest spills by the gfx950 listing: 4 for NT_DX_SNAKE -- 20-36 B against 144-160 B at 8 --,
+  // 8 for NT_DX0_SNAKE, whose partials of dW0 and da0 take the registers instead)
+  constexpr int EB0 = (MODE == NT_DX0_SNAKE) ? SIREN_SNAKE0_EB : SIREN_SNAKE_EB;
+  constexpr int EB = EB0 < SM ? EB0 : SM;
+  static_assert(SM % EB == 0, "Snake epilogue batches");
   uint4 cp_in[PRE_J > 0 ? PRE_J : 1][SN / 2];
+  uint4 ce_in[HAS_E ? EB : 1][2];
   float t_in[SM][2];
   auto pre = [&](int g) {
     int m0, n0;
@@ -254,6 +282,14 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp)
           cp_in[j][pp] = *(const uint4*)(p.Cprev + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
+      if constexpr (HAS_E) {
+#pragma unroll
+        for (int j = 0; j < EB; ++j) {
+          const size_t off = (size_t)(mrow0 + j * 16) * N + npc;
+          ce_in[j][0] = *(const uint4*)(p.Cprev + off);
+          ce_in[j][1] = *(const uint4*)(p.Eprev + off);
+        }
+      }
       if constexpr (nt_is_dx0(MODE)) {
 #pragma unroll
         for (int j = 0; j < SM; ++j) {
@@ -480,11 +516,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               }
             } else if constexpr (MODE == NT_FWD_SNAKE) {
               const float4 a4 = *(const float4*)(a_lds + nq + i * 16);
-              const float av[4] = {a4.x, a4.y, a4.z, a4.w};
+              const float4 ia4 = *(const float4*)(ia_lds + nq + i * 16);
+              const float av[4] = {a4.x, a4.y, a4.z, a4.w}, iav[4] = {ia4.x, ia4.y, ia4.z, ia4.w};
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float z = acc[i][j][r] + bb[r];
-                const float ia = 1.0f / av[r];
+                const float ia = iav[r];
                 const float x = __builtin_amdgcn_fractf((z * av[r]) * kInv2Pi);  // a z in revolutions
                 const float sn = __builtin_amdgcn_sinf(x), cn = __builtin_amdgcn_cosf(x);
                 const float s2 = sn * sn, sc2 = 2.0f * sn * cn;
@@ -551,61 +588,134 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int r = 0; r < 4; ++r) cs[q][i][r] = 0.f;
 
       const float om = p.omega;
-#pragma unroll
-      for (int j = 0; j < SM; ++j) {
-        const int m = mrow0 + j * 16;
-        const size_t rowoff = (size_t)m * N;
-        float t0 = 0.f, t1 = 0.f;
-        if constexpr (nt_is_dx0(MODE)) {
-          t0 = t_in[j][0];
-          t1 = t_in[j][1];
-        }
-#pragma unroll
-        for (int pp = 0; pp < SN / 2; ++pp) {
-          uint2 cpu[2];
-          const uint4 cpv = (j < PRE_J) ? cp_in[j < PRE_J ? j : 0][pp] : *(const uint4*)(p.Cprev + rowoff + npc + pp * 32);
-          unswap16_pair(cpv, cpu[0], cpu[1]);
-          uint2 epu[2];
-          if constexpr (MODE == NT_DX_SNAKE || MODE == NT_DX0_SNAKE)
-            unswap16_pair(*(const uint4*)(p.Eprev + rowoff + npc + pp * 32), epu[0], epu[1]);
-          uint2 dzp[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int i = 2 * pp + h;
-            const h16x4 cp = as_h4(cpu[h]);
-            float dz[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
-              cs[0][i][r] += dz[r];
-              if constexpr (nt_is_dx0(MODE)) {
-                cs[1][i][r] += dz[r] * t0;
-                cs[2][i][r] += dz[r] * t1;
-              }
-              if constexpr (MODE == NT_DX_SNAKE) cs[1][i][r] += acc[i][j][r] * (float)as_h4(epu[h])[r];
-              if constexpr (MODE == NT_DX0_SNAKE) cs[3][i][r] += acc[i][j][r] * (float)as_h4(epu[h])[r];
-            }
-            dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
-          }
-          if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE)
-            st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
-        }
-      }
       // partial layout: NT_DX [tm][N]; NT_DX0 [tm][1+in][N] with q=0 -> db0, q=1+j -> dW0[:, j];
-      // NT_DX_SNAKE [tm][2][N] with q=0 -> db, q=1 -> da
+      // NT_DX_SNAKE [tm][2][N] with q=0 -> db, q=1 -> da.  flush(i): column subtile i's partials
+      // over this wave's rows (DPP across the 16 row lanes) into the LDS scratch
+      auto flush = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (q >= nred) break;
-        // NT_DX0_SNAKE: da0 (slot 3) goes out as partial row 1 + in
-        const bool da0 = (MODE == NT_DX0_SNAKE) && q == nred - 1;
-#pragma unroll
-        for (int i = 0; i < SN; ++i) {
+        for (int q = 0; q < 4; ++q) {
+          if (q >= nred) break;
+          // NT_DX0_SNAKE: da0 (slot 3) goes out as partial row 1 + in
+          const bool da0 = (MODE == NT_DX0_SNAKE) && q == nred - 1;
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = row16_sum(da0 ? cs[3][i][r] : cs[q][i][r]);
           if ((lane & 15) == 0)
             *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + i * 16 + 4 * (lane >> 4)) =
                 float4{v[0], v[1], v[2], v[3]};
+        }
+      };
+      // the 16-B piece (row subtile j, column pair pp) from its Cprev (and Eprev) piece.  Each column
+      // partial sums its rows in order 0 .. SM-1 whatever order the pieces go in
+      auto piece = [&](auto jc, auto ppc, const uint4& cpv, const uint4& epv) {
+        constexpr int j = decltype(jc)::value, pp = decltype(ppc)::value;
+        const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
+        float t0 = 0.f, t1 = 0.f;
+        if constexpr (nt_is_dx0(MODE)) {
+          t0 = t_in[j][0];
+          t1 = t_in[j][1];
+        }
+        uint2 cpu[2];
+        unswap16_pair(cpv, cpu[0], cpu[1]);
+        uint2 epu[2];
+        if constexpr (HAS_E) unswap16_pair(epv, epu[0], epu[1]);
+        uint2 dzp[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = 2 * pp + h;
+          const h16x4 cp = as_h4(cpu[h]);
+          float dz[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
+            cs[0][i][r] += dz[r];
+            if constexpr (nt_is_dx0(MODE)) {
+              cs[1][i][r] += dz[r] * t0;
+              cs[2][i][r] += dz[r] * t1;
+            }
+            if constexpr (MODE == NT_DX_SNAKE) cs[1][i][r] += acc[i][j][r] * (float)as_h4(epu[h])[r];
+            if constexpr (MODE == NT_DX0_SNAKE) cs[3][i][r] += acc[i][j][r] * (float)as_h4(epu[h])[r];
+          }
+          dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
+        }
+        if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE)
+          st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+      };
+      if constexpr (HAS_E) {
+        static_assert(SN == 4, "two column pairs");
+        static_for<0, 2>([&](auto ppc) {
+          constexpr int pp = decltype(ppc)::value;
+          static_for<0, SM / EB>([&](auto bqc) {
+            constexpr int bq = decltype(bqc)::value;
+            if constexpr (pp == 0 && bq == 0) {
+              static_for<0, EB>([&](auto jc) { piece(jc, ppc, ce_in[decltype(jc)::value][0], ce_in[decltype(jc)::value][1]); });
+            } else {
+              uint4 cq[EB], eq[EB];
+#pragma unroll
+              for (int jj = 0; jj < EB; ++jj) {
+                const size_t off = (size_t)(mrow0 + (bq * EB + jj) * 16) * N + npc + pp * 32;
+                cq[jj] = *(const uint4*)(p.Cprev + off);
+                eq[jj] = *(const uint4*)(p.Eprev + off);
+              }
+              static_for<0, EB>([&](auto jc) {
+                constexpr int jj = decltype(jc)::value;
+                piece(std::integral_constant<int, bq * EB + jj>{}, ppc, cq[jj], eq[jj]);
+              });
+            }
+          });
+          flush(std::integral_constant<int, 2 * pp>{});  // this pair's column partials are final
+          flush(std::integral_constant<int, 2 * pp + 1>{});
+        });
+      } else {
+        // NT_DX / NT_DX0: rows in order, both column pairs of a row together (rows >= PRE_J loaded
+        // at use), then the column partials
+#pragma unroll
+        for (int j = 0; j < SM; ++j) {
+          const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
+          float t0 = 0.f, t1 = 0.f;
+          if constexpr (nt_is_dx0(MODE)) {
+            t0 = t_in[j][0];
+            t1 = t_in[j][1];
+          }
+#pragma unroll
+          for (int pp = 0; pp < SN / 2; ++pp) {
+            uint2 cpu[2];
+            const uint4 cpv =
+                (j < PRE_J) ? cp_in[j < PRE_J ? j : 0][pp] : *(const uint4*)(p.Cprev + rowoff + npc + pp * 32);
+            unswap16_pair(cpv, cpu[0], cpu[1]);
+            uint2 dzp[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int i = 2 * pp + h;
+              const h16x4 cp = as_h4(cpu[h]);
+              float dz[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
+                cs[0][i][r] += dz[r];
+                if constexpr (nt_is_dx0(MODE)) {
+                  cs[1][i][r] += dz[r] * t0;
+                  cs[2][i][r] += dz[r] * t1;
+                }
+              }
+              dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
+            }
+            if constexpr (MODE == NT_DX) st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q >= nred) break;
+#pragma unroll
+          for (int i = 0; i < SN; ++i) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[q][i][r]);
+            if ((lane & 15) == 0)
+              *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + i * 16 + 4 * (lane >> 4)) =
+                  float4{v[0], v[1], v[2], v[3]};
+          }
         }
       }
       lds_barrier();

@@ -19,6 +19,15 @@
 
 namespace siren {
 
+// f(integral_constant<int, I>) for I = B .. E-1, unrolled at compile time
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt immediate");

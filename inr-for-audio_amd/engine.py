@@ -334,10 +334,12 @@ class SirenEngine:
             order.append((i,) + span(ids))
         order.append((L,) + span([ix["W0"], ix["b0"]] + ([ix["a0"]] if ix["a0"] is not None else [])))
         self._events = []
-        for _ in range(L + 2):
-            ev = torch.cuda.Event()
-            ev.record()  # materialise the hipEvent_t so its handle can go to the C-ABI
-            self._events.append(ev)
+        with torch.cuda.device(self.device):  # events of the engine's device, whatever is current
+            for _ in range(L + 2):
+                ev = torch.cuda.Event()
+                # materialise the hipEvent_t so its handle can go to the C-ABI
+                ev.record(torch.cuda.current_stream(self.device))
+                self._events.append(ev)
         last = self.batches[-1]
         for k, ev in enumerate(self._events):
             last.grad_ready[k] = ev.cuda_event

@@ -50,12 +50,15 @@ def main():
     Cp = torch.cos(torch.rand(R, H, device=dev, generator=g) * 6.2831853).to(f16)
     dZ = (torch.randn(R, H, device=dev, generator=g) * 1e-2).to(f16)
     t = torch.linspace(-1, 1, R, device=dev).reshape(R, 1)
+    Ep = ((torch.rand(R, H, device=dev, generator=g) - 0.5) * 0.5).to(f16)  # a Snake layer's dY/da
+    a_snake = 0.5 + torch.rand(H, device=dev, generator=g)
     # zero-filled: the parity check compares whole buffers, including what a tile size leaves unwritten
     outs = {nm: {"Y": torch.zeros(R, H, dtype=f16, device=dev), "C": torch.zeros(R, H, dtype=f16, device=dev),
                  "hp": torch.zeros(H // 128, R, device=dev), "dZp": torch.zeros(R, H, dtype=f16, device=dev),
                  "part": torch.zeros(R // 128, 3, H, device=dev), "out": torch.zeros(R, device=dev),
                  "g": torch.zeros(R, device=dev), "sse": torch.zeros(R // 256, device=dev),
-                 "gsum": torch.zeros(R // 256, device=dev)} for nm in libs}
+                 "gsum": torch.zeros(R // 256, device=dev), "E": torch.zeros(R, H, dtype=f16, device=dev)}
+            for nm in libs}
     y = torch.sin(t[:, 0] * 2300.0) * 0.5
     bh = torch.zeros(1, device=dev)
     gs = torch.tensor([2.0 ** 9, 2.0 ** -9], device=dev)
@@ -83,6 +86,14 @@ def main():
         if kind == "dx0":
             return lambda: lib.siren_first_bwd_dx(P(dZ), P(WT), P(Cp), P(t), 1, ctypes.c_float(3000.0), R, H, None,
                                                   P(o["part"]), s())
+        if kind in ("dx_snake", "dx_tanh"):  # dX into a Snake / Tanh layer
+            act = 1 if kind == "dx_snake" else 2
+            return lambda: lib.siren_inner_bwd_dx_act(P(dZ), P(WT), P(Cp), P(Ep), act, ctypes.c_float(1.0), R, H,
+                                                      None, P(o["dZp"]), P(o["part"]), s())
+        if kind in ("fwd_snake", "fwd_tanh"):
+            act = 1 if kind == "fwd_snake" else 2
+            return lambda: lib.siren_inner_fwd_act(P(X), P(W), P(b), act, ctypes.c_float(1.0), P(a_snake), R, H,
+                                                   P(o["Y"]), P(o["C"]), P(o["E"]), None, None, P(tq), s())
         if kind == "dw":
             return lambda: lib.siren_inner_bwd_dw(P(X), P(dZ), R, H, splits, 0, P(slab), s())
         raise ValueError(kind)
@@ -106,6 +117,8 @@ def main():
                 torch.cuda.synchronize()
                 o = outs[nm]
                 got[nm] = {"fwd": (o["Y"], o["C"]), "fwd_head": (o["Y"], o["C"], o["hp"]), "dx": (o["dZp"], o["part"]),
+                           "dx_snake": (o["dZp"], o["part"]), "dx_tanh": (o["dZp"], o["part"]),
+                           "fwd_snake": (o["Y"], o["C"], o["E"]), "fwd_tanh": (o["Y"], o["C"]),
                            "dx0": (o["part"],), "fwd_hb": (o["out"], o["g"], o["sse"], o["dZp"], o["part"])}[k]
                 got[nm] = tuple(x.clone() for x in got[nm])
             for nm in libs:

@@ -25,9 +25,11 @@ def main():
     ap.add_argument("--pipes", default="-1,1")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rows", type=int, default=1 << 20)
+    ap.add_argument("--lib", default="", help="time this build of the library (path relative to the repo root)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    lib = _lib.load()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = _lib.load(os.path.join(root, args.lib)) if args.lib else _lib.load()
     n = args.rows
     t = torch.linspace(-1, 1, n).reshape(n, 1)
     y = 0.5 * torch.sin(2300.0 * t)
