@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--pipes", default="-1,1")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rows", type=int, default=1 << 20)
+    ap.add_argument("--breakdown", action="store_true", help="per-kind kernel ms per step (HIP events around "
+                    "every launch, untimed pass)")
     ap.add_argument("--lib", default="", help="time this build of the library (path relative to the repo root)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -47,6 +49,15 @@ def main():
                 eng.step()
             torch.cuda.synchronize()
             out[f"{name}_p{pipe}"] = (time.perf_counter() - t0) / args.steps * 1e3
+            if args.breakdown:
+                _lib.check(lib.siren_profile_enable(4096), "profile_enable")
+                for _ in range(args.steps):
+                    eng.step()
+                torch.cuda.synchronize()
+                for k, (ms, cnt) in _lib.profile_read().items():
+                    if cnt:
+                        out[f"{name}_p{pipe}:{k}"] = ms / args.steps
+                _lib.check(lib.siren_profile_enable(0), "profile_disable")
     lib.siren_set_option(2, -1)
     print(json.dumps({k: round(v, 3) for k, v in out.items()}))
 
