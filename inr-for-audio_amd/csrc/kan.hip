@@ -250,10 +250,18 @@ constexpr int KF_CST = KF_R + 4;   // [*][row] / [*][o] tiles of the backward
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ float f4(const float4& v, int t) { return t == 0 ? v.x : t == 1 ? v.y : t == 2 ? v.z : v.w; }
 
-// acc[j] += sum over ng groups of 16 k: A(16 rows at ap) x B(16 cols at bp + j * bstride)
-template <int NJ, int NA>
+// acc[j] += sum over ng groups of 16 k: A(16 rows at ap) x B(16 cols at bp + j * bstride).
+// Two accumulator sets (k-steps t = 0, 2 of a group into acc, t = 1, 3 into acc2, added at the
+// end in that fixed order): 2 NJ independent MFMA chains per wave.  With NJ = 4 chains the f32
+// MFMA's dependent-issue latency is exposed (tools/micro/mfma_f32_rate: 111 vs 146 TFLOP/s for 4
+// vs 9 chains at two waves per SIMD).  SPLIT = false keeps one set (the forward: measured no gain,
+// cfg5 kan_fwd 0.753 vs 0.778 ms per step; the backward products gain 4% of the step).
+template <int NJ, int NA, bool SPLIT = true>
 __device__ __forceinline__ void kf_mfma_groups(const float* ap, const float* bp, int bstride, int ng, f32x4 (&acc)[NA]) {
   static_assert(NJ <= NA, "more column tiles than accumulators");
+  f32x4 acc2[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float4 a = ld4(ap), b[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) b[j] = ld4(bp + j * bstride);
@@ -269,10 +277,17 @@ __device__ __forceinline__ void kf_mfma_groups(const float* ap, const float* bp,
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[j] = kf_mfma(f4(a, t), f4(b[j], t), acc[j]);
+      for (int j = 0; j < NJ; ++j) {
+        if (SPLIT && (t & 1)) acc2[j] = kf_mfma(f4(a, t), f4(b[j], t), acc2[j]);
+        else acc[j] = kf_mfma(f4(a, t), f4(b[j], t), acc[j]);
+      }
     a = an;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) b[j] = bn[j];
+  }
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] += acc2[j];
   }
 }
 
@@ -379,7 +394,7 @@ __global__ __launch_bounds__(256) void kan_fwd_fused_kernel(const float* __restr
     __syncthreads();
     if (vec && i0 + KF_IC < in) load_chunk(i0 + KF_IC);
     if ((KAN_ABL & 2) == 0)
-      kf_mfma_groups<4>(&As[16 * wv + li][4 * lk], &Ws[li][4 * lk], 16 * KF_AST, kpad >> 4, acc);
+      kf_mfma_groups<4, 4, false>(&As[16 * wv + li][4 * lk], &Ws[li][4 * lk], 16 * KF_AST, kpad >> 4, acc);
     __syncthreads();
   }
 #pragma unroll
