@@ -24,6 +24,12 @@
 #ifndef KAN_ABL
 #define KAN_ABL 0
 #endif
+// knot window of the basis recursion (kan_bases_window): 1 = span by counting + an 8-knot gather
+// from the LDS knot row (cfg5 2.249 -> 2.202 ms per step), 0 = per-span predicate with the window
+// captured by selects (kept for the head kernels, whose lanes hold one input's knots throughout)
+#ifndef KAN_WINDOW_GATHER
+#define KAN_WINDOW_GATHER 1
+#endif
 
 namespace siren {
 
@@ -62,14 +68,34 @@ __device__ __forceinline__ float kan_div(float a, float d, float y) {
 
 // The recursion on the window: s (the span, -1 outside the grid), w[q] = B[s-3+q] and, with
 // DERIV, d[q] = B'[s-3+q] (q = 0..3).
-template <bool DERIV, bool RCP>
+template <bool DERIV, bool RCP, bool GATHER = (KAN_WINDOW_GATHER != 0)>
 __device__ __forceinline__ int kan_bases_window(float x, const float* __restrict__ g, float* w, float* d,
                                                 const float* __restrict__ inv) {
+  int s = -1;
+  float kw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+if constexpr (GATHER) {
+  // span by counting: for non-decreasing knots, g[s] <= x < g[s+1] holds exactly for
+  // s = #{j : g[j] <= x} - 1 when that count is 1 .. NG-1 (x below the first knot, at or past the
+  // last one, or NaN: no span), the same s as the per-span predicate below.  The window is then
+  // one gather of 8 knots from the LDS row g (indices clamped into the array; the entries a clamp
+  // touches belong to terms the recursion discards)
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < KAN_NG; ++j) cnt += (x >= g[j]) ? 1 : 0;
+  s = (cnt >= 1 && cnt <= KAN_NG - 1) ? cnt - 1 : -1;
+  {
+    const int s0 = s < 0 ? 0 : s;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int t = s0 - 3 + e;
+      t = t < 0 ? 0 : (t > KAN_NG - 1 ? KAN_NG - 1 : t);
+      kw[e] = g[t];
+    }
+  }
+  } else {
   float kn[KAN_NG];
 #pragma unroll
   for (int j = 0; j < KAN_NG; ++j) kn[j] = g[j];
-  int s = -1;
-  float kw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < KAN_NG - 1; ++j) {
     const bool hit = x >= kn[j] && x < kn[j + 1];
@@ -79,6 +105,7 @@ __device__ __forceinline__ int kan_bases_window(float x, const float* __restrict
       const int t = j - 3 + e;
       if (t >= 0 && t < KAN_NG) kw[e] = hit ? kn[t] : kw[e];
     }
+  }
   }
   // window w[q] = B[s - 3 + q], q = 0..3, plus w[4] = B[s + 1] = 0
   float ww[5] = {0.0f, 0.0f, 0.0f, 1.0f, 0.0f}, dd[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -118,7 +145,7 @@ __device__ __forceinline__ int kan_bases_window(float x, const float* __restrict
   return s;
 }
 
-template <bool DERIV, bool RCP = false>
+template <bool DERIV, bool RCP = false, bool GATHER = (KAN_WINDOW_GATHER != 0)>
 __device__ __forceinline__ void kan_bases_local(float x, const float* __restrict__ g, float* b, float* db,
                                                 const float* __restrict__ inv = nullptr) {
 #pragma unroll
@@ -129,7 +156,7 @@ __device__ __forceinline__ void kan_bases_local(float x, const float* __restrict
     return;
   }
   float w[4], d[4];
-  const int s = kan_bases_window<DERIV, RCP>(x, g, w, d, inv);
+  const int s = kan_bases_window<DERIV, RCP, GATHER>(x, g, w, d, inv);
   if (s < 0) return;
 #pragma unroll
   for (int c = 0; c < KAN_NB; ++c) {
@@ -147,6 +174,14 @@ __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 __device__ __forceinline__ float silu_grad(float x) {
   const float s = 1.0f / (1.0f + expf(-x));
   return s * (1.0f + x * (1.0f - s));
+}
+// silu(x) and silu_grad(x) on one exp: the same values as the two calls (same operations on the
+// same 1 + exp(-x))
+__device__ __forceinline__ void silu_and_grad(float x, float& sl, float& dsl) {
+  const float d = 1.0f + expf(-x);
+  sl = x / d;
+  const float s = 1.0f / d;
+  dsl = s * (1.0f + x * (1.0f - s));
 }
 
 // ---- fused layer kernels --------------------------------------------------------------------
@@ -432,7 +467,7 @@ __global__ __launch_bounds__(256) void kan_head_fwd_kernel(const float* __restri
     if (on) {
       const float x = X[n * in + lane];
       float b[KAN_NB], unused[KAN_NB];
-      kan_bases_local<false>(x, gk[lane], b, unused, inv[lane]);
+      kan_bases_local<false, false, false>(x, gk[lane], b, unused, inv[lane]);  // lane-fixed knots: selects
       v = silu(x) * wb;
 #pragma unroll
       for (int c = 0; c < KAN_NB; ++c) v += b[c] * ws[c];
@@ -478,7 +513,7 @@ __global__ __launch_bounds__(256) void kan_head_train_kernel(const float* __rest
     float x = 0.f, v = 0.f, sl = 0.f, b[KAN_NB], db[KAN_NB];
     if (on) {
       x = X[n * in + lane];
-      kan_bases_local<true>(x, gk[lane], b, db, inv[lane]);
+      kan_bases_local<true, false, false>(x, gk[lane], b, db, inv[lane]);  // lane-fixed knots: selects
       sl = silu(x);
       v = sl * wb;
 #pragma unroll
@@ -802,8 +837,7 @@ __global__ __launch_bounds__(KB_THREADS) void kan_bwd_fused_kernel(const float* 
         if (r0 + r < re) {
           const float x = Xs[r][ii];
           kan_bases_local<true, true>(x, gk[ii], b, dbs[h]);
-          sl = silu(x);
-          dsl[h] = silu_grad(x);
+          silu_and_grad(x, sl, dsl[h]);
         }
         AD[ii * KF_CST + r] = sl;
 #pragma unroll
