@@ -427,8 +427,19 @@ __device__ __forceinline__ void col_reduce_block(const float* __restrict__ part,
   const int r0 = (int)(((int64_t)chunk * nrows) / nchunk);
   const int r1 = (int)(((int64_t)(chunk + 1) * nrows) / nchunk);
   float s = 0.f;
-  if (col < ncols)
-    for (int r = r0 + rg; r < r1; r += 4) s += part[(int64_t)r * row_stride + col];
+  if (col < ncols) {
+    // rows r0 + rg, r0 + rg + 4, ... summed in that order; 8 loads in flight ahead of the adds
+    // (one dependent load per row made pass 1 latency-bound)
+    int r = r0 + rg;
+    for (; r + 28 < r1; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(r + 4 * u) * row_stride + col];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; r < r1; r += 4) s += part[(int64_t)r * row_stride + col];
+  }
   red[rg][threadIdx.x & 63] = s;
   __syncthreads();
   if (rg == 0 && col < ncols) {
