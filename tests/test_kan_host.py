@@ -64,3 +64,31 @@ def test_kan_oracle_matches_reference():
         r = f[f"k64_grad_{k}"]
         rel = np.linalg.norm(gr.reshape(r.shape) - r) / np.linalg.norm(r)
         assert rel < 1e-4, (k, rel)
+
+
+def test_span_by_count_equals_span_predicate():
+    """kan.hip kan_bases_window (KAN_WINDOW_GATHER): for non-decreasing knots the span found by
+    counting, s = #{j : g[j] <= x} - 1 if that count is 1 .. 11 else -1, equals the span of the
+    per-span predicate g[j] <= x < g[j+1] (kan.py:94-96's order-0 bases), for x on, between and
+    outside the knots, +-inf and NaN, on uniform grids (efficient-KAN init) and on sorted grids
+    with repeated knots (what update_grid can produce)."""
+    rng = np.random.default_rng(0)
+    grids = [(np.arange(-3, 9, dtype=np.float32) * np.float32(0.4) - np.float32(1.0))]
+    for _ in range(40):
+        g = np.sort(rng.normal(size=12).astype(np.float32))
+        if rng.random() < 0.5:  # repeated knots
+            k = rng.integers(0, 11)
+            g[k + 1] = g[k]
+        grids.append(g)
+    for g in grids:
+        xs = np.concatenate([g, np.nextafter(g, np.float32(np.inf)), np.nextafter(g, np.float32(-np.inf)),
+                             rng.uniform(g[0] - 1, g[-1] + 1, 200).astype(np.float32),
+                             np.array([np.inf, -np.inf, np.nan], dtype=np.float32)])
+        for x in xs:
+            s_pred = -1
+            for j in range(11):
+                if g[j] <= x < g[j + 1]:
+                    s_pred = j
+            cnt = int(np.sum(x >= g))
+            s_cnt = cnt - 1 if 1 <= cnt <= 11 else -1
+            assert s_cnt == s_pred, (g, x)
