@@ -115,10 +115,12 @@ inline hipError_t mark_ready(const siren_batch* b, int k, hipStream_t s) {
 
 // one segment of a multi-segment column reduction (capi's sets never exceed kMaxColSegs)
 inline void seg_add(ColSegs& sg, const float* src, float* out, int out_stride = 1) {
-  sg.src[sg.n] = src;
-  sg.out[sg.n] = out;
-  sg.out_stride[sg.n] = out_stride;
-  ++sg.n;
+  if (sg.n < kMaxColSegs) {
+    sg.src[sg.n] = src;
+    sg.out[sg.n] = out;
+    sg.out_stride[sg.n] = out_stride;
+  }
+  ++sg.n;  // a set past kMaxColSegs is rejected by col_reduce_multi
 }
 
 // SIREN_OPT_HEAD_FUSE: siren_train_step runs the last layer as NT_FWD_HB when it can

@@ -100,6 +100,14 @@ def _hip_check_layer(lay: "KANLinear"):
         raise NotImplementedError("HIP KAN path: grid_size=5, spline_order=3 (kan.py defaults)")
     if not lay.enable_standalone_scale_spline or not isinstance(lay.base_activation, torch.nn.SiLU):
         raise NotImplementedError("HIP KAN path: SiLU base and a standalone spline scaler")
+    # kan.hip finds a basis span by counting knots <= x, which equals kan.py:94-96's span predicate
+    # for non-decreasing knots (kan.py's grids always are; checked once per grid version)
+    key = (lay.grid.data_ptr(), lay.grid._version)
+    if getattr(lay, "_knots_checked", None) != key:
+        g = lay.grid
+        if not bool((g[:, 1:] >= g[:, :-1]).all()):
+            raise NotImplementedError("HIP KAN path: every input's knots must be non-decreasing")
+        lay._knots_checked = key
 
 
 def _kan_splits(rows: int) -> int:

@@ -92,3 +92,20 @@ def test_span_by_count_equals_span_predicate():
             cnt = int(np.sum(x >= g))
             s_cnt = cnt - 1 if 1 <= cnt <= 11 else -1
             assert s_cnt == s_pred, (g, x)
+
+
+def test_hip_path_rejects_unsorted_knots():
+    """The HIP KAN path counts knots to find a span, which needs non-decreasing knots: a grid
+    that is not is rejected before any launch; after the grid is restored the layer passes."""
+    from inr_for_audio_amd import kan as hk
+    torch.manual_seed(0)
+    lay = hk.KANLinear(4, 3)
+    hk._hip_check_layer(lay)
+    keep = lay.grid.clone()
+    with torch.no_grad():
+        lay.grid[2, 5], lay.grid[2, 6] = lay.grid[2, 6].item(), lay.grid[2, 5].item()
+    with pytest.raises(NotImplementedError, match="non-decreasing"):
+        hk._hip_check_layer(lay)
+    with torch.no_grad():
+        lay.grid.copy_(keep)
+    hk._hip_check_layer(lay)
