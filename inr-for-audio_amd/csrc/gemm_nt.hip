@@ -669,7 +669,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         });
       } else {
         // NT_DX / NT_DX0: rows in order, both column pairs of a row together (rows >= PRE_J loaded
-        // at use), then the column partials
+        // at use), then the column partials.  The same arithmetic as `piece`, kept as a plain loop:
+        // written through the lambda, NT_DX0 takes 252-256 VGPRs instead of 239-244 (gfx950 listing)
 #pragma unroll
         for (int j = 0; j < SM; ++j) {
           const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
