@@ -175,7 +175,46 @@ _DXFL_NEW2 = """          if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE) dz
 _DWL2_OLD = """        const int ks = ks_begin + min(kt, nkl - 1);  // past the slice: a consumed piece re-read"""
 _DWL2_NEW = """        const int ks = ks_begin + (min(kt, nkl - 1) & 7);"""
 
+# MFMA issue order inside a ping-pong phase: column subtile (X fragment) outer, so consecutive MFMAs
+# share their B operand instead of their A operand (every accumulator keeps its k order:
+# bit-identical) -- operand toggling between consecutive MFMAs, timing only
+_ORD_OLD = """#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int il = 0; il < 2; ++il)
+#pragma unroll
+          for (int jl = 0; jl < 4; ++jl) {
+            const h16x8 a = NH ? wf1[il][kk] : wf0[il][kk];"""
+_ORD_NEW = """#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int jl = 0; jl < 4; ++jl)
+#pragma unroll
+          for (int il = 0; il < 2; ++il) {
+            const h16x8 a = NH ? wf1[il][kk] : wf0[il][kk];"""
+_TNORD_OLD = """#pragma unroll
+        for (int il = 0; il < 8; ++il)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[il][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8[il], b4[j], acc[il][j], 0, 0, 0);"""
+_TNORD_NEW = """#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int il = 0; il < 8; ++il)
+            acc[il][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8[il], b4[j], acc[il][j], 0, 0, 0);"""
+
+# the same, serpentine: every consecutive pair of MFMAs shares one operand, across the column
+# subtiles and across the two k32 halves (per-accumulator k order unchanged: bit-identical)
+_ORD2_NEW = """#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const int kk = t >> 3, u = t & 7, jq = u >> 1;
+        const int jl = kk ? 3 - jq : jq;
+        const int il = ((t >> 1) & 1) ? 1 - (u & 1) : (u & 1);
+            const h16x8 a = NH ? wf1[il][kk] : wf0[il][kk];"""
+
 VARIANTS = {
+    "ord2": {"gemm_nt.hip": [(_ORD_OLD, _ORD2_NEW)]},
+    "ord": {"gemm_nt.hip": [(_ORD_OLD, _ORD_NEW)], "gemm_tn.hip": [(_TNORD_OLD, _TNORD_NEW)]},
     "dw_l2": {"gemm_tn.hip": [(_DWL2_OLD, _DWL2_NEW)]},
     "dxfl": {"gemm_nt.hip": [(_DXFL_OLD1, _DXFL_NEW1), (_DXFL_OLD2, _DXFL_NEW2)]},
     "fl_dxfl": {"gemm_nt.hip": [(_FL_OLD, _FL_NEW), (_DXFL_OLD1, _DXFL_NEW1), (_DXFL_OLD2, _DXFL_NEW2)]},
