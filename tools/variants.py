@@ -212,7 +212,16 @@ _ORD2_NEW = """#pragma unroll
         const int il = ((t >> 1) & 1) ? 1 - (u & 1) : (u & 1);
             const h16x8 a = NH ? wf1[il][kk] : wf0[il][kk];"""
 
+# dW two-segment MFMA order, serpentine over (il, j): consecutive MFMAs share an operand across
+# the il boundaries too (bit-identical) -- timing only
+_TNSERP_NEW = """#pragma unroll
+        for (int t = 0; t < 32; ++t) {
+          const int il = t >> 2, jq = t & 3, j = (il & 1) ? 3 - jq : jq;
+          acc[il][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8[il], b4[j], acc[il][j], 0, 0, 0);
+        }"""
+
 VARIANTS = {
+    "tnserp": {"gemm_tn.hip": [(_TNORD_OLD, _TNSERP_NEW)]},
     "ord2": {"gemm_nt.hip": [(_ORD_OLD, _ORD2_NEW)]},
     "ord": {"gemm_nt.hip": [(_ORD_OLD, _ORD_NEW)], "gemm_tn.hip": [(_TNORD_OLD, _TNORD_NEW)]},
     "dw_l2": {"gemm_tn.hip": [(_DWL2_OLD, _DWL2_NEW)]},
