@@ -71,3 +71,40 @@ def test_batched_shadow_cast_matches_per_layer_cast():
         torch.cuda.synchronize()
         assert torch.equal(Wh.view(torch.int16), eng.Wh[i].view(torch.int16)), i
         assert torch.equal(WTh.view(torch.int16), eng.WTh[i].view(torch.int16)), i
+
+
+@pytest.mark.parametrize("mask_all", [True, False])
+def test_profile_records_count_launches(mask_all):
+    """ABI 10: the run of back-to-back plain forward launches is one profiling record, and
+    siren_profile_read still returns the launch count (bench.py's per-launch average divides by
+    it).  A 2^17 x 256 SIREN with 3 hidden layers: 2 plain forwards + the fused last layer per
+    step, 3 dX launches... per kind, launches = steps x launches per step."""
+    lib = _lib.load()
+    torch.manual_seed(0)
+    model = SirenWithSnakeTanh(1, 1, H, 3, 0, 0, first_omega_0=300.0, hidden_omega_0=30.0)
+    t = torch.linspace(-1, 1, 1 << 17).reshape(-1, 1)
+    eng = SirenEngine(model, t, torch.sin(9.0 * t[:, 0]), device=DEV)
+    L = eng.spec.n_inner
+    eng.step()
+    torch.cuda.synchronize()
+    kinds = _lib.PROF_KINDS
+    mask = 0xFFFFFFFF if mask_all else (1 << kinds.index("inner_fwd"))
+    _lib.check(lib.siren_profile_mask(mask), "mask")
+    _lib.check(lib.siren_profile_enable(4096), "enable")
+    try:
+        steps = 3
+        for _ in range(steps):
+            eng.step()
+        torch.cuda.synchronize()
+        pr = _lib.profile_read()
+    finally:
+        _lib.check(lib.siren_profile_enable(0), "disable")
+        _lib.check(lib.siren_profile_mask(0xFFFFFFFF), "mask")
+    fused = pr["head_fwd"][1] > 0 if mask_all else lib.siren_nt_tile(1 << 17, H) == 256
+    n_fwd = pr["inner_fwd"][1]
+    assert n_fwd == steps * (L - 1 if fused else L), pr
+    assert pr["inner_fwd"][0] > 0
+    if mask_all:
+        assert pr["bwd_dw"][1] == steps * L and pr["bwd_dx"][1] == steps * (L - 1) and pr["bwd_dx0"][1] == steps
+    else:
+        assert all(n == 0 for k, (ms, n) in pr.items() if k != "inner_fwd")
