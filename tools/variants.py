@@ -220,7 +220,21 @@ _TNSERP_NEW = """#pragma unroll
           acc[il][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8[il], b4[j], acc[il][j], 0, 0, 0);
         }"""
 
+# ping-pong K-loops without the s_setprio around each MFMA cluster (the barriers alone order the
+# two wave groups; bit-identical) -- timing only
+_PRIO_OLD1 = """      __builtin_amdgcn_s_setprio(1);
+      mma(ph);       // each MFMA waits (counted lgkmcnt) only for its fragments
+      wait_lgkm0();  // every read of this slot has landed before the barrier that frees it
+      __builtin_amdgcn_s_setprio(0);"""
+_PRIO_NEW1 = """      mma(ph);
+      wait_lgkm0();"""
+_PRIO_OLD2 = """      __builtin_amdgcn_s_setprio(1);
+      mma(sg);
+      __builtin_amdgcn_s_setprio(0);"""
+_PRIO_NEW2 = """      mma(sg);"""
+
 VARIANTS = {
+    "noprio": {"gemm_pipeline.h": [(_PRIO_OLD1, _PRIO_NEW1), (_PRIO_OLD2, _PRIO_NEW2)]},
     "tnserp": {"gemm_tn.hip": [(_TNORD_OLD, _TNSERP_NEW)]},
     "ord2": {"gemm_nt.hip": [(_ORD_OLD, _ORD2_NEW)]},
     "ord": {"gemm_nt.hip": [(_ORD_OLD, _ORD_NEW)], "gemm_tn.hip": [(_TNORD_OLD, _TNORD_NEW)]},
