@@ -23,6 +23,7 @@ import argparse
 import json
 import os
 import platform
+import re
 import sys
 import time
 
@@ -47,21 +48,27 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-KIND_MATCH = {  # profile kind -> (kernel-name substring, accepted template-argument tails)
-    # gemm_nt_kernel<Cfg, MODE, HEAD[, QUEUE]>: the head-less forward, statically walked or
-    # from the dynamic tile queue (gemm_nt.hip)
-    "inner_fwd": ("gemm_nt_kernel", (", 0, false>", ", 0, false, true>")),
-    "bwd_dx": ("gemm_nt_kernel", (", 1, false>", ", 1, false, true>")),
-    "bwd_dx0": ("gemm_nt_kernel", (", 2, false>", ", 2, false, true>")),
-    "bwd_dw": ("gemm_tn_kernel", ("",)),
+KIND_MATCH = {  # profile kind -> (kernel-name substring, (MODE, HEAD) of gemm_nt_kernel or None)
+    # gemm_nt_kernel<Cfg, MODE, HEAD[, QUEUE]>: statically walked (QUEUE false) or from the
+    # dynamic tile queue (gemm_nt.hip); QUEUE is not part of the kind
+    "inner_fwd": ("gemm_nt_kernel", ("0", "false")),
+    "bwd_dx": ("gemm_nt_kernel", ("1", "false")),
+    "bwd_dx0": ("gemm_nt_kernel", ("2", "false")),
+    "bwd_dw": ("gemm_tn_kernel", None),
     # NT_FWD_HB: the last layer fused with the head, the loss gradient and the head backward
-    "head_fwd": ("gemm_nt_kernel", (", 7, true>",)),
+    "head_fwd": ("gemm_nt_kernel", ("7", "true")),
 }
+_NT_ARGS = re.compile(r"gemm_nt_kernel<siren::NtCfg<[^>]*>, (\d+), (true|false)(?:, (?:true|false))?>")
 
 
 def kind_match(kind: str, kernel_name: str) -> bool:
-    a, tails = KIND_MATCH[kind]
-    return a in kernel_name and any(t in kernel_name for t in tails)
+    a, mode_head = KIND_MATCH[kind]
+    if a not in kernel_name:
+        return False
+    if mode_head is None:
+        return True
+    m = _NT_ARGS.search(kernel_name)
+    return m is not None and (m.group(1), m.group(2)) == mode_head
 
 
 def pmc_traffic(kind: str):

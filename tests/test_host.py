@@ -181,3 +181,22 @@ def test_package_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in src.replace("# oracle", ""), f
+
+
+def test_bench_kernel_kinds_cover_every_template_form():
+    """bench.py maps rocprof kernel names to launch kinds for the roofline's PMC fields: every
+    gemm_nt_kernel<Cfg, MODE, HEAD[, QUEUE]> form the library instantiates must resolve to exactly
+    one kind (a dX launch with QUEUE = false once fell through and left `traffic` null)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    cfg = "void siren::gemm_nt_kernel<siren::NtCfg<256, 256, 2, 4, 64, 2, true>, {}>(siren::NtParams)"
+    want = {"0, false": "inner_fwd", "0, false, true": "inner_fwd", "0, false, false": "inner_fwd",
+            "1, false": "bwd_dx", "1, false, false": "bwd_dx", "1, false, true": "bwd_dx",
+            "2, false, false": "bwd_dx0", "7, true, false": "head_fwd", "7, true": "head_fwd",
+            "3, false, false": None}
+    for args, kind in want.items():
+        hits = [k for k in bench.KIND_MATCH if bench.kind_match(k, cfg.format(args))]
+        assert hits == ([kind] if kind else []), (args, hits)
+    tn = "void siren::gemm_tn_kernel<siren::TnCfg<256, 256, 2, 4, 64, 2, 2> >(siren::TnParams)"
+    assert [k for k in bench.KIND_MATCH if bench.kind_match(k, tn)] == ["bwd_dw"]
