@@ -125,8 +125,8 @@ inline void seg_add(ColSegs& sg, const float* src, float* out, int out_stride = 
 
 // SIREN_OPT_HEAD_FUSE: siren_train_step runs the last layer as NT_FWD_HB when it can
 int g_head_fuse = 1;
-bool head_fused(const siren_net* n, const siren_batch* b) {
-  return g_head_fuse && n->act[n->n_inner - 1] == SIREN_ACT_SINE && gemm_nt_head_fusable(b->rows, n->hidden);
+bool head_fused(const siren_net* n, const siren_batch* b, hipStream_t s) {
+  return g_head_fuse && n->act[n->n_inner - 1] == SIREN_ACT_SINE && gemm_nt_head_fusable(b->rows, n->hidden, s);
 }
 
 // forward through all layers + head partials; returns hip status.  hb: the last layer is the
@@ -355,7 +355,7 @@ int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b
 
   // mean backward: MSELoss 2 err / N, L1Loss sign(err) / N
   const float gfac = (float)((b->loss_mode == 1 ? 1.0 : 2.0) / b->n_total);
-  const bool hb = head_fused(net, b);
+  const bool hb = head_fused(net, b, s);
   if (hb) {
     // the fused head needs the backward scale S before the forward: from the bound of max|g|
     // (elementwise.hip grad_scale_bound) instead of the step's max|g|
@@ -498,7 +498,7 @@ int siren_head_fused_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, 
   if (!hidden_ok(hidden) || rows <= 0 || rows % 256 || n_valid < 0 || n_valid > rows || !(n_total > 0))
     return SIREN_ERR_SHAPE;
   if (loss_mode < 0 || loss_mode > 1 || !(head_omega >= 0.f)) return SIREN_ERR_CONFIG;
-  if (!gemm_nt_head_fusable(rows, hidden)) return SIREN_ERR_CONFIG;
+  if (!gemm_nt_head_fusable(rows, hidden, S(stream))) return SIREN_ERR_CONFIG;
   NtParams p = {};
   p.X = B(X); p.W = B(Wh); p.M = rows; p.N = hidden; p.K = hidden;
   p.tile = nt_choose_tile(rows, hidden);

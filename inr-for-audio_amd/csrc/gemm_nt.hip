@@ -126,6 +126,9 @@ constexpr bool nt_is_dx0(int m) { return m == NT_DX0 || m == NT_DX0_SNAKE; }
 
 // NT_FWD_HB: head_part word not yet published by its column tile's block (launch_nt fills it)
 constexpr unsigned kHeadPending = 0xFFFFFFFFu;
+// polls (s_sleep 1 = 64 clocks each, ~1-1.4 s in all) before a hand-off wait gives up; a partner
+// normally publishes within one tile period (~40 us)
+constexpr int kHeadSpinLimit = 1 << 25;
 
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
@@ -379,9 +382,17 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           float v = own;
           if (jt != tn) {
             unsigned u;
+            int polls = 0;
             while ((u = __hip_atomic_load(hpu + (size_t)jt * p.M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
-                   kHeadPending)
+                   kHeadPending) {
+              // bounded: a partner kept off the chip (CUs held by another process) turns the band's
+              // loss into NaN -- a loud failure of the step -- instead of hanging the launch
+              if (++polls > kHeadSpinLimit) {
+                u = 0x7fc00000u;
+                break;
+              }
               __builtin_amdgcn_s_sleep(1);
+            }
             v = __uint_as_float(u);
           }
           o += v;
@@ -896,6 +907,10 @@ static int stream_cus(hipStream_t s) {
   return g_num_cus[dev];
 }
 
+// NT_FWD_HB co-residency: blocks per CU for the fused kernel x CUs >= grid (queried once per device)
+static int g_hb_per_cu[64] = {};
+static bool hb_coresident(int grid, hipStream_t s);
+
 template <class Cfg, int MODE, bool HEAD>
 static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent) {
   // the static ping-pong schedule assumes an even number (>= 2) of K-tiles per tile
@@ -914,11 +929,20 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
     // for each other's head partials.  Blocks are dispatched in order, so a waiting block's
     // partners are resident or next in line (at most tiles_n - 1 blocks per XCD wait on blocks
     // not yet dispatched while every fully resident band group runs on).
+    // Co-residency: every block of the grid must be resident at once on an idle device (the
+    // launcher checks the occupancy; the caller falls back to the unfused launches when it fails),
+    // and the wait itself is bounded (kHeadSpinLimit), so CUs taken by other work can slow the
+    // hand-off or fail the step loudly, never hang it.  G is rounded down to a multiple of
+    // 8 * tiles_n when the grid allows it, so that the G/8 blocks xcd_remap deals to each XCD hold
+    // whole band groups: a band's tiles then share one L2.
     static_assert(Cfg::PP, "fused head: ping-pong persistent walk");
     const int tiles_n = p.N / Cfg::BN;
     if (p.diag || tiles_n > 4 || p.M % Cfg::BM) return hipErrorInvalidValue;
-    int g = grid - grid % tiles_n;
+    int g = grid;
+    if (g >= 8 * tiles_n) g -= g % (8 * tiles_n);
+    else g -= g % tiles_n;
     if (g < tiles_n) g = tiles_n;
+    if (!hb_coresident(g, s)) return hipErrorCooperativeLaunchTooLarge;
     const hipError_t e = hipMemsetAsync(p.head_part, 0xFF, (size_t)tiles_n * p.M * sizeof(float), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD>), dim3(g), dim3(Cfg::THREADS), 0, s, p);
@@ -936,6 +960,19 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
   }
   hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD>), dim3(grid), dim3(Cfg::THREADS), 0, s, p);
   return hipGetLastError();
+}
+
+static bool hb_coresident(int grid, hipStream_t s) {
+  int dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (dev < 0 || dev >= 64) return false;
+  if (g_hb_per_cu[dev] == 0) {
+    int n = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, reinterpret_cast<const void*>(&gemm_nt_kernel<NtLargePP, NT_FWD_HB, true>), NtLargePP::THREADS, 0);
+    g_hb_per_cu[dev] = (e == hipSuccess && n > 0) ? n : -1;
+  }
+  return g_hb_per_cu[dev] > 0 && (long)g_hb_per_cu[dev] * stream_cus(s) >= grid;
 }
 
 template <class Cfg>
@@ -987,14 +1024,18 @@ int nt_choose_tile(int M, int N) {
   return (long)(M / 256) * (N / 256) >= 512 ? 256 : 128;
 }
 
-bool gemm_nt_head_fusable(int M, int N) {
-  return nt_choose_tile(M, N) == 256 && nt_pp() && M % 256 == 0 && N % 256 == 0 && N / 256 <= 4 && N % 128 == 0;
+bool gemm_nt_head_fusable(int M, int N, hipStream_t s) {
+  if (!(nt_choose_tile(M, N) == 256 && nt_pp() && M % 256 == 0 && N % 256 == 0 && N / 256 <= 4 && N % 128 == 0))
+    return false;
+  // the grid launch_nt will use must be co-resident (one block per CU on an idle device)
+  const int ntiles = (M / 256) * (N / 256), cap = g_nt_grid_cap > 0 ? g_nt_grid_cap : stream_cus(s);
+  return hb_coresident(ntiles < cap ? ntiles : cap, s);
 }
 
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (p.M % NtSmall::BM || p.N % NtSmall::BN || p.K % NtSmall::BK || p.M <= 0 || p.N > NtSmall::MAXN) return hipErrorInvalidValue;
   if (mode == NT_FWD_HB) {
-    if (!head || p.tile != 256 || !gemm_nt_head_fusable(p.M, p.N)) return hipErrorInvalidValue;
+    if (!head || p.tile != 256 || !gemm_nt_head_fusable(p.M, p.N, s)) return hipErrorInvalidValue;
     if (!p.head_w || !p.head_part || !p.gscale || !p.dZ || !p.colsum_part || !p.b_head || !p.out || !p.g ||
         !p.sse_part || !p.gsum_part || (p.n_valid > 0 && !p.target))
       return hipErrorInvalidValue;

@@ -64,7 +64,8 @@ constexpr int kTileqInts = 768;  // == SIREN_TILEQ_INTS (include/siren_hip.h)
 int nt_choose_tile(int M, int N);
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s);
 // NT_FWD_HB is available for this shape under the current tile / K-loop settings
-bool gemm_nt_head_fusable(int M, int N);
+// also false when the fused launch's grid could not be co-resident (occupancy x CUs < grid)
+bool gemm_nt_head_fusable(int M, int N, hipStream_t s);
 void gemm_nt_set_tile(int tile);  // 0 = auto, 128, 256 (A/B measurement)
 void gemm_tn_set_tile(int tile);
 void gemm_nt_set_pipe(int v);     // 256x256 K-loop: 4 ping-pong (default), 1 persistent, 0 one tile per block
