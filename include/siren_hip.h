@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 10
+#define SIREN_ABI_VERSION 11
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 /* ints in one tile-queue counter set (siren_batch.tileq, siren_inner_fwd's tileq): the
@@ -152,7 +152,13 @@ typedef struct siren_batch {
   void* grad_ready[SIREN_MAX_INNER + 2];
   /* run.py:161-169 loss_mode: 0 = MSELoss (sse = sum err^2, g = 2 err / n_total), 1 = L1Loss
    * ('mae': sse slot = sum |err|, g = sign(err) / n_total) */
-  int32_t loss_mode, pad1;
+  int32_t loss_mode;
+  /* ABI 11: 1 = gmax_part holds the max|g| partials of a previous siren_train_step /
+   * siren_backward on this workspace (same rows).  A Snake last layer then runs fused with the
+   * head (the backward scale S must be fixed before the forward, and |Y_L| has no bound, so S is
+   * taken from those partials; the range guard catches a step whose |g| outgrew it).  0: a Snake
+   * last layer runs unfused.  Sine / Tanh last layers ignore it. */
+  int32_t head_scale_prev;
   const siren_guard* guard;  /* range guard (NULL: fixed headroom 6, no overflow recovery) */
   int32_t* tileq;            /* SIREN_TILEQ_INTS ints of tile-queue counters on the device of the
                                 activations (NULL: the forward GEMM's static tile walk) */
@@ -219,6 +225,17 @@ int siren_head_fused_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, 
                          int32_t n_valid, double n_total, int32_t loss_mode, const float* gscale, float* head_part,
                          float* out, float* g, float* sse_part, float* gsum_part, uint16_t* dZ, float* part,
                          void* stream);
+/* ABI 11: siren_head_fused_fwd for a last inner layer of any kind (act, siren_act): SINE as
+ * siren_head_fused_fwd; SNAKE (models.py:235-241, a = its [hidden] a) and TANH (models.py:366-372)
+ * with their derivative in place of the cosine (omega unused) -- dZ, out, g and the partials as
+ * siren_inner_fwd_act -> siren_head_loss -> siren_head_bwd compute them at the same gscale;
+ * part[rows/256][2][hidden] (db_L, dw_head), Snake part[rows/256][3][hidden] (+ da_L);
+ * gmax_part (nullable): [rows/256] max|g| per 256 rows, as siren_head_loss writes it */
+int siren_head_fused_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, int32_t act, float omega,
+                             const float* a, int32_t rows, int32_t hidden, const float* w_head, const float* b_head,
+                             float head_omega, const float* y, int32_t n_valid, double n_total, int32_t loss_mode,
+                             const float* gscale, float* head_part, float* out, float* g, float* sse_part,
+                             float* gsum_part, float* gmax_part, uint16_t* dZ, float* part, void* stream);
 /* the fused head's backward scale, fixed before the forward: gscale = {S, 1/S} from a bound of
  * max|g| (MSE: (sum|w_head| + |b_head| + max|y|) 2/n_total, or 1 + max|y| through a final sine of
  * head_omega; L1: 1/n_total; x head_omega) x max|w_head| x act_bound (|dY/dz| bound of the last

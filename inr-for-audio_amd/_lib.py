@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 MAX_INNER = 16
 ROW_TILE = 128
 TILEQ_INTS = 768  # SIREN_TILEQ_INTS: one tile-queue counter set
@@ -79,7 +79,7 @@ class SirenBatch(ctypes.Structure):
         ("gmax_part", _p), ("gscale", _p), ("col_part", _p), ("col_part2", _p), ("red_tmp", _p), ("slab", _p),
         ("E", _p * (MAX_INNER + 1)),
         ("grad_ready", _p * (MAX_INNER + 2)),
-        ("loss_mode", _i32), ("pad1", _i32), ("guard", _p), ("tileq", _p),
+        ("loss_mode", _i32), ("head_scale_prev", _i32), ("guard", _p), ("tileq", _p),
     ]
 
 
@@ -150,6 +150,9 @@ _SIGS = {
     "siren_cast_weight": (ctypes.c_int, [_p, _i32, _i32, _p, _p, _p]),
     "siren_head_fused_fwd": (ctypes.c_int, [_p, _p, _p, ctypes.c_float, _i32, _i32, _p, _p, ctypes.c_float, _p, _i32,
                                             ctypes.c_double, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "siren_head_fused_fwd_act": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_float, _p, _i32, _i32, _p, _p,
+                                                ctypes.c_float, _p, _i32, ctypes.c_double, _i32, _p, _p, _p, _p, _p,
+                                                _p, _p, _p, _p, _p]),
     "siren_grad_scale_bound": (ctypes.c_int, [_p, _i32, _p, _p, _p, _i32, ctypes.c_double, ctypes.c_float, _i32,
                                               ctypes.c_float, _p, _p]),
     "siren_set_option": (ctypes.c_int, [_i32, _i32]),

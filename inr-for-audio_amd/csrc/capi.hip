@@ -123,10 +123,19 @@ inline void seg_add(ColSegs& sg, const float* src, float* out, int out_stride = 
   ++sg.n;  // a set past kMaxColSegs is rejected by col_reduce_multi
 }
 
-// SIREN_OPT_HEAD_FUSE: siren_train_step runs the last layer as NT_FWD_HB when it can
+// the fused last-layer mode of a last inner layer kind
+int hb_mode(int act) {
+  return act == SIREN_ACT_SNAKE ? NT_FWD_HB_SNAKE : (act == SIREN_ACT_TANH ? NT_FWD_HB_TANH : NT_FWD_HB);
+}
+// SIREN_OPT_HEAD_FUSE: siren_train_step runs the last layer as NT_FWD_HB* when it can.  A Snake last
+// layer needs a backward scale before its forward that no bound gives tightly (|Y| is not bounded
+// by 1): it fuses only when the caller says gmax_part holds a previous launch's max|g| partials
+// (siren_batch.head_scale_prev); the range guard catches a step whose |g| outgrew that scale.
 int g_head_fuse = 1;
 bool head_fused(const siren_net* n, const siren_batch* b, hipStream_t s) {
-  return g_head_fuse && n->act[n->n_inner - 1] == SIREN_ACT_SINE && gemm_nt_head_fusable(b->rows, n->hidden, s);
+  const int act = n->act[n->n_inner - 1];
+  if (!g_head_fuse || (act == SIREN_ACT_SNAKE && !b->head_scale_prev)) return false;
+  return gemm_nt_head_fusable(b->rows, n->hidden, s, hb_mode(act));
 }
 
 // forward through all layers + head partials; returns hip status.  hb: the last layer is the
@@ -165,8 +174,9 @@ hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s, bool h
       p.sse_part = b->sse_part; p.gsum_part = b->gsum_part;
       p.n_valid = b->n_valid; p.loss_mode = b->loss_mode; p.gfac = gfac; p.head_omega = n->head_omega;
       p.gscale = b->gscale; p.dZ = B(b->dZ[0]); p.colsum_part = b->col_part;
+      p.gmax_part = b->gmax_part;  // this launch's max|g|: the next one's scale (Snake last layer)
       close_run();
-      SIREN_PROF(SIREN_PROF_HEAD_FWD, s, gemm_nt(NT_FWD_HB, true, p, s));
+      SIREN_PROF(SIREN_PROF_HEAD_FWD, s, gemm_nt(hb_mode(n->act[i]), true, p, s));
       continue;
     }
     if (run == 0) prof_begin(SIREN_PROF_INNER_FWD, s);
@@ -265,10 +275,13 @@ static int run_backward(const siren_net* net, const siren_grads* gr, siren_batch
   const int ntile = nt_choose_tile(R, H), tntile = tn_choose_tile(R, H, H);
   const int prow = R / ntile;  // partial rows written by the NT_DX / NT_DX0 epilogues
   if (hb) {
+    // [R/256][2][H] partials of db_L, dw_head; a Snake last layer [R/256][3][H] with da_L
+    const bool snake_last = net->act[L - 1] == SIREN_ACT_SNAKE;
     ColSegs sg = {};
     seg_add(sg, b->col_part + H, gr->w_head);
     seg_add(sg, b->col_part, gr->b[L - 1]);
-    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce_multi(sg, 2 * H, prow, H, 1, b->red_tmp, s));
+    if (snake_last) seg_add(sg, b->col_part + 2 * H, gr->a[L - 1]);
+    SIREN_PROF(SIREN_PROF_REDUCE, s, col_reduce_multi(sg, (snake_last ? 3 : 2) * H, prow, H, 1, b->red_tmp, s));
   } else {
     const bool snake_last = net->act[L - 1] == SIREN_ACT_SNAKE;
     float* da_last = b->col_part + (int64_t)(R / 128) * H;  // second H-wide slab of col_part
@@ -357,13 +370,20 @@ int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b
   const float gfac = (float)((b->loss_mode == 1 ? 1.0 : 2.0) / b->n_total);
   const bool hb = head_fused(net, b, s);
   if (hb) {
-    // the fused head needs the backward scale S before the forward: from the bound of max|g|
-    // (elementwise.hip grad_scale_bound) instead of the step's max|g|
+    // the fused head needs the backward scale S before the forward.  Sine / Tanh last layer
+    // (|Y_L| <= 1): from the bound of max|g| (elementwise.hip grad_scale_bound) instead of the
+    // step's max|g|.  Snake: from the previous launch's max|g| partials in gmax_part (grad_scale,
+    // the unfused path's own scale rule on last step's g)
     const int L = net->n_inner, nv = b->n_valid, nyp = (nv + 255) / 256;
-    if (nv > 0) SIREN_PROF(SIREN_PROF_HEAD, s, gmax_partials(b->target, nv, b->gmax_part, s));
-    SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale_bound(b->gmax_part, nyp, net->w_head, net->b_head, H, gfac,
-                                                    net->head_omega, b->loss_mode, act_bound(net, L - 1),
-                                                    b->gscale, s, (const GuardState*)b->guard));
+    if (net->act[L - 1] == SIREN_ACT_SNAKE) {
+      SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale(b->gmax_part, (R + 255) / 256, net->w_head, H, act_bound(net, L - 1),
+                                                b->gscale, s, (const GuardState*)b->guard));
+    } else {
+      if (nv > 0) SIREN_PROF(SIREN_PROF_HEAD, s, gmax_partials(b->target, nv, b->gmax_part, s));
+      SIREN_PROF(SIREN_PROF_HEAD, s, grad_scale_bound(b->gmax_part, nyp, net->w_head, net->b_head, H, gfac,
+                                                      net->head_omega, b->loss_mode, act_bound(net, L - 1),
+                                                      b->gscale, s, (const GuardState*)b->guard));
+    }
   }
   // ---- forward (models.py:388-394) + MSE / L1 (run.py:161-169) ----
   SIREN_TRY(run_forward(net, b, s, hb, gfac));
@@ -507,6 +527,30 @@ int siren_head_fused_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, 
   p.n_valid = n_valid; p.loss_mode = loss_mode; p.gfac = (float)((loss_mode == 1 ? 1.0 : 2.0) / n_total);
   p.head_omega = head_omega; p.gscale = gscale; p.dZ = B(dZ); p.colsum_part = part;
   return (int)gemm_nt(NT_FWD_HB, true, p, S(stream));
+}
+
+int siren_head_fused_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, int32_t act, float omega,
+                             const float* a, int32_t rows, int32_t hidden, const float* w_head, const float* b_head,
+                             float head_omega, const float* y, int32_t n_valid, double n_total, int32_t loss_mode,
+                             const float* gscale, float* head_part, float* out, float* g, float* sse_part,
+                             float* gsum_part, float* gmax_part, uint16_t* dZ, float* part, void* stream) {
+  if (!X || !Wh || !b || !w_head || !b_head || !gscale || !head_part || !out || !g || !sse_part || !gsum_part ||
+      !dZ || !part || (n_valid > 0 && !y) || (act == SIREN_ACT_SNAKE && !a))
+    return SIREN_ERR_NULL;
+  if (!hidden_ok(hidden) || rows <= 0 || rows % 256 || n_valid < 0 || n_valid > rows || !(n_total > 0))
+    return SIREN_ERR_SHAPE;
+  if (act < SIREN_ACT_SINE || act > SIREN_ACT_TANH || loss_mode < 0 || loss_mode > 1 || !(head_omega >= 0.f))
+    return SIREN_ERR_CONFIG;
+  if (!gemm_nt_head_fusable(rows, hidden, S(stream), hb_mode(act))) return SIREN_ERR_CONFIG;
+  NtParams p = {};
+  p.X = B(X); p.W = B(Wh); p.M = rows; p.N = hidden; p.K = hidden;
+  p.tile = nt_choose_tile(rows, hidden);
+  p.omega = omega; p.bias = b; p.act_a = a; p.head_w = w_head; p.head_part = head_part;
+  p.target = y; p.b_head = b_head; p.out = out; p.g = g; p.sse_part = sse_part; p.gsum_part = gsum_part;
+  p.gmax_part = gmax_part;
+  p.n_valid = n_valid; p.loss_mode = loss_mode; p.gfac = (float)((loss_mode == 1 ? 1.0 : 2.0) / n_total);
+  p.head_omega = head_omega; p.gscale = gscale; p.dZ = B(dZ); p.colsum_part = part;
+  return (int)gemm_nt(hb_mode(act), true, p, S(stream));
 }
 
 int siren_grad_scale_bound(const float* y, int32_t n_valid, float* ymax_part, const float* w_head,

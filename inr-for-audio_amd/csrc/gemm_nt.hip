@@ -98,8 +98,8 @@ struct NtLds {
   static constexpr int BIAS = Cfg::RING + Cfg::RED;
   static constexpr int HW = BIAS + (nt_is_fwd(MODE) ? Cfg::VEC : 0);
   static constexpr int A = HW + (HEAD ? Cfg::VEC : 0);
-  static constexpr int IA = A + (MODE == NT_FWD_SNAKE ? Cfg::VEC : 0);   // Snake 1/a, divided once
-  static constexpr int QS = IA + (MODE == NT_FWD_SNAKE ? Cfg::VEC : 0);  // dynamic tile queue: 2 tile ids
+  static constexpr int IA = A + (nt_is_snake_fwd(MODE) ? Cfg::VEC : 0);   // Snake 1/a, divided once
+  static constexpr int QS = IA + (nt_is_snake_fwd(MODE) ? Cfg::VEC : 0);  // dynamic tile queue: 2 tile ids
   static constexpr int SIZE = QS + 16;
   static_assert(SIZE <= 160 * 1024, "LDS");
 };
@@ -135,7 +135,7 @@ template <class Cfg, int MODE>
 constexpr int epilogue_stores() {
   return (MODE == NT_FWD || MODE == NT_FWD_TANH) ? Cfg::SM * Cfg::SN
          : MODE == NT_FWD_SNAKE                 ? 3 * Cfg::SM * Cfg::SN / 2
-         : (MODE == NT_DX || MODE == NT_DX_SNAKE || MODE == NT_FWD_HB) ? Cfg::SM * Cfg::SN / 2
+         : (MODE == NT_DX || MODE == NT_DX_SNAKE || nt_is_hb(MODE)) ? Cfg::SM * Cfg::SN / 2
                                                   : 0;
 }
 
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     for (int c = tid * 4; c < N; c += Cfg::THREADS * 4) {
       *(float4*)(bias_lds + c) = *(const float4*)(p.bias + c);
       if constexpr (HEAD) *(float4*)(hw_lds + c) = *(const float4*)(p.head_w + c);
-      if constexpr (MODE == NT_FWD_SNAKE) {
+      if constexpr (nt_is_snake_fwd(MODE)) {
         const float4 a4 = *(const float4*)(p.act_a + c);
         *(float4*)(a_lds + c) = a4;
         *(float4*)(ia_lds + c) = float4{1.0f / a4.x, 1.0f / a4.y, 1.0f / a4.z, 1.0f / a4.w};
@@ -310,13 +310,19 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     const int npc = n0 + wn * TN + swap16_col(lane);      // swapped layout: this lane's piece
     const int mrow0 = m0 + wm * TM + (lane & 15);
 
-    if constexpr (MODE == NT_FWD_HB) {
-      // ---- phase 1: Y = sin, C = cos of the tile rounded to fp16 as NT_FWD stores them, packed
-      // IN PLACE of their accumulators (4 fp32 -> 4 + 4 fp16: the same 4 VGPRs, so nothing more is
-      // live across the hand-off than the accumulators themselves), and the head partial of the
-      // band's rows over this column tile, summed exactly as NT_FWD + HEAD sums it
+    if constexpr (nt_is_hb(MODE)) {
+      // The last hidden layer fused with the head, the loss gradient and the head backward, for
+      // the three last-layer kinds (models.py:114-115, 235-241, 366-372).
+      // ---- phase 1: the layer's outputs for the head partial of the band's rows over this column
+      // tile, summed exactly as NT_FWD(_SNAKE/_TANH) + HEAD sums them.  Sine / Tanh: Y and C (= cos,
+      // or 1 - Y^2) rounded to fp16 as the unfused forward stores them, packed IN PLACE of their
+      // accumulators (4 fp32 -> 4 + 4 fp16: the same 4 VGPRs, so nothing more is live across the
+      // hand-off than the accumulators).  Snake has three fp16 outputs (Y, D, E), which do not fit
+      // there: the accumulators stay as they are and phase 2 re-evaluates the same expressions
+      // (bit-identical: the same operations on the same operands).
+      constexpr bool SNK = MODE == NT_FWD_HB_SNAKE, TNH = MODE == NT_FWD_HB_TANH;
       const int nq = n0 + wn * TN + 4 * (lane >> 4);
-      const float xs = p.omega * kInv2Pi;
+      const float xs = (MODE == NT_FWD_HB) ? p.omega * kInv2Pi : 1.0f;
       float4 bias[SN], hw[SN];
 #pragma unroll
       for (int i = 0; i < SN; ++i) {
@@ -325,6 +331,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         hw[i] = *(const float4*)(hw_lds + nq + i * 16);
       }
       float hp[SM];
+      uint2 e16[SNK ? SN : 1][SNK ? SM : 1];  // Snake: fp16 E of the tile
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
         hp[j] = 0.f;
@@ -335,18 +342,48 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int h = 0; h < 2; ++h) {
             const int i = 2 * pp + h;
             const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
-            float sv[4], cv[4];
+            float sv[4];
+            if constexpr (SNK) {
+              const float4 a4 = *(const float4*)(a_lds + nq + i * 16);
+              const float4 ia4 = *(const float4*)(ia_lds + nq + i * 16);
+              const float av[4] = {a4.x, a4.y, a4.z, a4.w}, iav[4] = {ia4.x, ia4.y, ia4.z, ia4.w};
+              float cv[4], ev[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
-              sv[r] = __builtin_amdgcn_sinf(x);
-              cv[r] = __builtin_amdgcn_cosf(x);
+              for (int r = 0; r < 4; ++r) {
+                const float z = acc[i][j][r] + bb[r];
+                const float ia = iav[r];
+                const float x = __builtin_amdgcn_fractf((z * av[r]) * kInv2Pi);  // a z in revolutions
+                const float sn = __builtin_amdgcn_sinf(x), cn = __builtin_amdgcn_cosf(x);
+                const float s2 = sn * sn, sc2 = 2.0f * sn * cn;
+                sv[r] = z + s2 * ia;               // models.py:241
+                cv[r] = 1.0f + sc2;                // dY/dz
+                ev[r] = (z * sc2 - s2 * ia) * ia;  // dY/da
+              }
+              // Y and D packed in place of the accumulators, E beside them (2 VGPRs per 4 elements)
+              const uint2 yv = as_u2(pack4(sv[0], sv[1], sv[2], sv[3])), cw = as_u2(pack4(cv[0], cv[1], cv[2], cv[3]));
+              acc[i][j] = __builtin_bit_cast(f32x4, uint4{yv.x, yv.y, cw.x, cw.y});
+              e16[i][j] = as_u2(pack4(ev[0], ev[1], ev[2], ev[3]));
+              asm volatile("" : "+v"(acc[i][j]), "+v"(e16[i][j]));
+            } else {
+              float cv[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                if constexpr (TNH) {
+                  const float y = tanhf(acc[i][j][r] + bb[r]);
+                  sv[r] = y;
+                  cv[r] = 1.0f - y * y;
+                } else {
+                  const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
+                  sv[r] = __builtin_amdgcn_sinf(x);
+                  cv[r] = __builtin_amdgcn_cosf(x);
+                }
+              }
+              const uint2 yv = as_u2(pack4(sv[0], sv[1], sv[2], sv[3])), cw = as_u2(pack4(cv[0], cv[1], cv[2], cv[3]));
+              acc[i][j] = __builtin_bit_cast(f32x4, uint4{yv.x, yv.y, cw.x, cw.y});
+              // opaque: the packing happens here (left to itself the compiler sinks the cos past the
+              // hand-off into phase 2, keeping the fp32 arguments live across it: 372 B of spills)
+              asm volatile("" : "+v"(acc[i][j]));
             }
-            const uint2 yv = as_u2(pack4(sv[0], sv[1], sv[2], sv[3])), cw = as_u2(pack4(cv[0], cv[1], cv[2], cv[3]));
-            acc[i][j] = __builtin_bit_cast(f32x4, uint4{yv.x, yv.y, cw.x, cw.y});
-            // opaque: the packing happens here (left to itself the compiler sinks the cos past the
-            // hand-off into phase 2, keeping the fp32 arguments live across it: 372 B of spills)
-            asm volatile("" : "+v"(acc[i][j]));
             hp[j] += sv[0] * hw[i].x + sv[1] * hw[i].y + sv[2] * hw[i].z + sv[3] * hw[i].w;
           }
         }
@@ -367,7 +404,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       // head_loss for the band's rows.  The partial itself is the flag: head_part is filled with
       // kHeadPending before the launch and a published value is never that pattern (NaN is
       // stored canonical), so no fence orders it -- one agent-scope atomic word each way.
-      float* g_lds = red + WN * BM;
+      // g_lds sits past the column-partial scratch of phase 2 (3 partial rows with Snake)
+      float* g_lds = red + (SNK ? 3 * Cfg::WM * BN : WN * BM);
       float e2 = 0.f, gv = 0.f;
       if (tid < BM) {
         float own = 0.f;
@@ -418,26 +456,32 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         }
       }
       // the band's loss and bias-gradient partials (head_loss_kernel's 256-row blocks and sums;
-      // threads >= BM add zeros); the block sums' barriers also publish g_lds
+      // threads >= BM add zeros); the block sums' barriers also publish g_lds.  max|g| of the band
+      // (head_loss_kernel's gmax partial): the next launch's backward scale for a Snake last layer
       const float se = block_sum(e2, g_lds + BM);
       const float gs = block_sum(gv, g_lds + BM);
+      float gx = 0.f;
+      if (p.gmax_part) gx = block_max(fabsf(gv), g_lds + BM);
       if (tn == 0 && tid == 0) {
         p.sse_part[tm] = se;
         p.gsum_part[tm] = gs;
+        if (p.gmax_part) p.gmax_part[tm] = gx;
       }
-      // ---- phase 2: head_bwd_kernel on the registers: dz = ((g w) C) omega stored x S, column
-      // partials of dz (db_L) and of g Y (dw_head) over the tile's rows
-      // column pairs outermost (the 16-B dZ pieces pair adjacent subtiles), rows inside: each
-      // pair's accumulators and column partials die before the next pair's begin
-      const float om = p.omega, S = p.gscale[0];
+      // ---- phase 2: head_bwd_kernel on the registers: dz = ((g w) C) omega stored x S (omega 1 for
+      // Snake / Tanh: C is their derivative), column partials of dz (db_L), of g Y (dw_head) and,
+      // Snake, of (g w) E (da_L) over the tile's rows.  Column pairs outermost (the 16-B dZ pieces
+      // pair adjacent subtiles), rows inside: each pair's accumulators and column partials die
+      // before the next pair's begin
+      constexpr int NQ = SNK ? 3 : 2;
+      const float om = (MODE == NT_FWD_HB) ? p.omega : 1.0f, S = p.gscale[0];
       float gm[SM];
 #pragma unroll
       for (int j = 0; j < SM; ++j) gm[j] = g_lds[wm * TM + j * 16 + (lane & 15)];
 #pragma unroll
       for (int pp = 0; pp < SN / 2; ++pp) {
-        float cs[2][2][4];  // [db_L, dw_head][subtile h][column r]
+        float cs[NQ][2][4];  // [db_L, dw_head, da_L][subtile h][column r]
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < NQ; ++q)
 #pragma unroll
           for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -450,15 +494,26 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             const int i = 2 * pp + h;
             const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);
             const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+            float cf[4], yf[4], ef[4];
             const uint4 pk = __builtin_bit_cast(uint4, acc[i][j]);
             const h16x4 yh = as_h4(uint2{pk.x, pk.y}), ch = as_h4(uint2{pk.z, pk.w});
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              yf[r] = (float)yh[r];
+              cf[r] = (float)ch[r];
+            }
+            if constexpr (SNK) {
+              const h16x4 eh = as_h4(e16[SNK ? i : 0][SNK ? j : 0]);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) ef[r] = (float)eh[r];
+            }
             float d[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float c = (float)ch[r], y = (float)yh[r];
-              const float dz = ((gm[j] * wv[r]) * c) * om;
+              const float dz = ((gm[j] * wv[r]) * cf[r]) * om;
               cs[0][h][r] += dz;
-              cs[1][h][r] += gm[j] * y;
+              cs[1][h][r] += gm[j] * yf[r];
+              if constexpr (SNK) cs[2][h][r] += (gm[j] * wv[r]) * ef[r];
               d[r] = dz * S;
             }
             dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
@@ -466,7 +521,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
         }
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
+        for (int q = 0; q < NQ; ++q)
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             float v[4];
@@ -480,11 +535,11 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       lds_barrier();
       if (tid < BN) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < NQ; ++q) {
           float sum = 0.f;
 #pragma unroll
           for (int w = 0; w < Cfg::WM; ++w) sum += red[(q * Cfg::WM + w) * BN + tid];
-          p.colsum_part[((size_t)tm * 2 + q) * N + n0 + tid] = sum;
+          p.colsum_part[((size_t)tm * NQ + q) * N + n0 + tid] = sum;
         }
       }
     } else if constexpr (nt_is_fwd(MODE)) {
@@ -908,8 +963,8 @@ static int stream_cus(hipStream_t s) {
 }
 
 // NT_FWD_HB co-residency: blocks per CU for the fused kernel x CUs >= grid (queried once per device)
-static int g_hb_per_cu[64] = {};
-static bool hb_coresident(int grid, hipStream_t s);
+static int g_hb_per_cu[3][64] = {};
+static bool hb_coresident(int mode, int grid, hipStream_t s);
 
 template <class Cfg, int MODE, bool HEAD>
 static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent) {
@@ -923,7 +978,7 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
   // the queue's shards are blockIdx % 8: every shard must have blocks
   // (measured: the forward gains 3-4%; dX is unchanged and dX0 loses 2%, its K-loop spills)
   const bool want = g_nt_queue == 2 || (g_nt_queue == 1 && nt_is_fwd(MODE));
-  if constexpr (MODE == NT_FWD_HB) {
+  if constexpr (nt_is_hb(MODE)) {
     // the static walk g = bp + i G with G a multiple of tiles_n: the tiles_n column tiles of a row
     // band are tile i of tiles_n consecutive blocks (one XCD under the xcd_remap order), which wait
     // for each other's head partials.  Blocks are dispatched in order, so a waiting block's
@@ -942,13 +997,13 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
     if (g >= 8 * tiles_n) g -= g % (8 * tiles_n);
     else g -= g % tiles_n;
     if (g < tiles_n) g = tiles_n;
-    if (!hb_coresident(g, s)) return hipErrorCooperativeLaunchTooLarge;
+    if (!hb_coresident(MODE, g, s)) return hipErrorCooperativeLaunchTooLarge;
     const hipError_t e = hipMemsetAsync(p.head_part, 0xFF, (size_t)tiles_n * p.M * sizeof(float), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD>), dim3(g), dim3(Cfg::THREADS), 0, s, p);
     return hipGetLastError();
   }
-  if constexpr (Cfg::PP && MODE != NT_FWD_HB) {
+  if constexpr (Cfg::PP && !nt_is_hb(MODE)) {
     if (p.tileq && want && !p.diag && grid % 8 == 0) {
       // the counter set starts every launch at zero, ordered on the launch's own stream
       // (graph capture records the memset as a node before the kernel)
@@ -962,17 +1017,20 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
   return hipGetLastError();
 }
 
-static bool hb_coresident(int grid, hipStream_t s) {
+static bool hb_coresident(int mode, int grid, hipStream_t s) {
   int dev = 0;
   if (hipStreamGetDevice(s, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) dev = 0;
-  if (dev < 0 || dev >= 64) return false;
-  if (g_hb_per_cu[dev] == 0) {
+  if (dev < 0 || dev >= 64 || !nt_is_hb(mode)) return false;
+  int& per_cu = g_hb_per_cu[mode - NT_FWD_HB][dev];
+  if (per_cu == 0) {
+    const void* fn = mode == NT_FWD_HB         ? reinterpret_cast<const void*>(&gemm_nt_kernel<NtLargePP, NT_FWD_HB, true>)
+                     : mode == NT_FWD_HB_SNAKE ? reinterpret_cast<const void*>(&gemm_nt_kernel<NtLargePP, NT_FWD_HB_SNAKE, true>)
+                                               : reinterpret_cast<const void*>(&gemm_nt_kernel<NtLargePP, NT_FWD_HB_TANH, true>);
     int n = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, reinterpret_cast<const void*>(&gemm_nt_kernel<NtLargePP, NT_FWD_HB, true>), NtLargePP::THREADS, 0);
-    g_hb_per_cu[dev] = (e == hipSuccess && n > 0) ? n : -1;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, NtLargePP::THREADS, 0);
+    per_cu = (e == hipSuccess && n > 0) ? n : -1;
   }
-  return g_hb_per_cu[dev] > 0 && (long)g_hb_per_cu[dev] * stream_cus(s) >= grid;
+  return per_cu > 0 && (long)per_cu * stream_cus(s) >= grid;
 }
 
 template <class Cfg>
@@ -1024,21 +1082,23 @@ int nt_choose_tile(int M, int N) {
   return (long)(M / 256) * (N / 256) >= 512 ? 256 : 128;
 }
 
-bool gemm_nt_head_fusable(int M, int N, hipStream_t s) {
+bool gemm_nt_head_fusable(int M, int N, hipStream_t s, int mode) {
   if (!(nt_choose_tile(M, N) == 256 && nt_pp() && M % 256 == 0 && N % 256 == 0 && N / 256 <= 4 && N % 128 == 0))
     return false;
   // the grid launch_nt will use must be co-resident (one block per CU on an idle device)
   const int ntiles = (M / 256) * (N / 256), cap = g_nt_grid_cap > 0 ? g_nt_grid_cap : stream_cus(s);
-  return hb_coresident(ntiles < cap ? ntiles : cap, s);
+  return hb_coresident(mode, ntiles < cap ? ntiles : cap, s);
 }
 
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (p.M % NtSmall::BM || p.N % NtSmall::BN || p.K % NtSmall::BK || p.M <= 0 || p.N > NtSmall::MAXN) return hipErrorInvalidValue;
-  if (mode == NT_FWD_HB) {
-    if (!head || p.tile != 256 || !gemm_nt_head_fusable(p.M, p.N, s)) return hipErrorInvalidValue;
+  if (nt_is_hb(mode)) {
+    if (!head || p.tile != 256 || !gemm_nt_head_fusable(p.M, p.N, s, mode)) return hipErrorInvalidValue;
     if (!p.head_w || !p.head_part || !p.gscale || !p.dZ || !p.colsum_part || !p.b_head || !p.out || !p.g ||
-        !p.sse_part || !p.gsum_part || (p.n_valid > 0 && !p.target))
+        !p.sse_part || !p.gsum_part || (p.n_valid > 0 && !p.target) || (mode == NT_FWD_HB_SNAKE && !p.act_a))
       return hipErrorInvalidValue;
+    if (mode == NT_FWD_HB_SNAKE) return launch_nt<NtLargePP, NT_FWD_HB_SNAKE, true>(p, s, true);
+    if (mode == NT_FWD_HB_TANH) return launch_nt<NtLargePP, NT_FWD_HB_TANH, true>(p, s, true);
     return launch_nt<NtLargePP, NT_FWD_HB, true>(p, s, true);
   }
   if (nt_is_dx0(mode) && (p.in_dim < 1 || p.in_dim > 2)) return hipErrorInvalidValue;
@@ -1051,7 +1111,7 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
     if (p.tile != 128) return hipErrorInvalidValue;
     return dispatch_dx0_snake<NtSmall>(p, s, false);
   }
-  if (mode >= NT_FWD_SNAKE) {
+  if (mode >= NT_FWD_SNAKE && mode <= NT_DX_SNAKE) {
     if ((mode == NT_FWD_SNAKE && (!p.act_a || !p.E)) || (mode == NT_DX_SNAKE && !p.Eprev))
       return hipErrorInvalidValue;
     if (p.tile == 256) {

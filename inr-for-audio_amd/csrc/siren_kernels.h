@@ -14,9 +14,14 @@ typedef _Float16 h16;  // activation / weight-shadow / gradient storage (fp16, s
 // of db0, dW0 (x t_j) and da0 = sum acc * E0
 // NT_FWD_HB: the last hidden SineLayer fused with the head, the loss gradient and the head backward
 // (training only): writes dZ_L x S instead of Y_L / C_L (see gemm_nt.hip)
+// NT_FWD_HB_SNAKE / NT_FWD_HB_TANH: the same for a Linear + Snake / Linear + Tanh last layer
+// (run.py:30's default train() stack ends in Snake layers)
 enum NtMode { NT_FWD = 0, NT_DX = 1, NT_DX0 = 2, NT_FWD_SNAKE = 3, NT_FWD_TANH = 4, NT_DX_SNAKE = 5,
-              NT_DX0_SNAKE = 6, NT_FWD_HB = 7 };
-constexpr bool nt_is_fwd(int m) { return m == NT_FWD || m == NT_FWD_SNAKE || m == NT_FWD_TANH || m == NT_FWD_HB; }
+              NT_DX0_SNAKE = 6, NT_FWD_HB = 7, NT_FWD_HB_SNAKE = 8, NT_FWD_HB_TANH = 9 };
+constexpr bool nt_is_hb(int m) { return m == NT_FWD_HB || m == NT_FWD_HB_SNAKE || m == NT_FWD_HB_TANH; }
+constexpr bool nt_is_fwd(int m) { return m == NT_FWD || m == NT_FWD_SNAKE || m == NT_FWD_TANH || nt_is_hb(m); }
+// forward modes that evaluate a Snake (they stage a and 1/a in LDS)
+constexpr bool nt_is_snake_fwd(int m) { return m == NT_FWD_SNAKE || m == NT_FWD_HB_SNAKE; }
 
 struct NtParams {
   const h16* X;  // [M][K]
@@ -47,9 +52,10 @@ struct NtParams {
   // ping-pong K-loop only: caller-owned tile-queue counter set of kTileqInts ints (null = the
   // static walk b, b + G, ...); gemm_nt zeroes it on the stream before each queue launch
   int* tileq;
-  // NT_FWD_HB (with head_w / head_part; gscale = {S, 1/S} set beforehand by grad_scale_bound;
-  // dZ = dZ_L x S; colsum_part [M/256][2][N] = partials of db_L and dw_head): head_loss's inputs
-  // and outputs for the band's rows
+  // NT_FWD_HB* (with head_w / head_part; gscale = {S, 1/S} set beforehand by grad_scale_bound, or
+  // for a Snake last layer by grad_scale from the previous launch's max|g|; dZ = dZ_L x S;
+  // colsum_part [M/256][2][N] = partials of db_L and dw_head, Snake [M/256][3][N] + da_L):
+  // head_loss's inputs and outputs for the band's rows
   const float* target;  // [M]
   const float* b_head;  // [1]
   float* out;           // [M]
@@ -58,6 +64,7 @@ struct NtParams {
   float* gsum_part;     // [M/256]
   int n_valid, loss_mode;
   float gfac, head_omega;
+  float* gmax_part;     // [M/256] max|g| per band (NT_FWD_HB*; null = not written)
 };
 constexpr int kTileqInts = 768;  // == SIREN_TILEQ_INTS (include/siren_hip.h)
 
@@ -65,7 +72,7 @@ int nt_choose_tile(int M, int N);
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s);
 // NT_FWD_HB is available for this shape under the current tile / K-loop settings
 // also false when the fused launch's grid could not be co-resident (occupancy x CUs < grid)
-bool gemm_nt_head_fusable(int M, int N, hipStream_t s);
+bool gemm_nt_head_fusable(int M, int N, hipStream_t s, int mode = NT_FWD_HB);
 void gemm_nt_set_tile(int tile);  // 0 = auto, 128, 256 (A/B measurement)
 void gemm_tn_set_tile(int tile);
 void gemm_nt_set_pipe(int v);     // 256x256 K-loop: 4 ping-pong (default), 1 persistent, 0 one tile per block

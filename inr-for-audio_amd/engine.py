@@ -358,6 +358,11 @@ class SirenEngine:
         for b in self.batches:
             check(self.lib.siren_train_step(ctypes.byref(self.net), ctypes.byref(self.grad_struct),
                                             ctypes.byref(b), s), "siren_train_step")
+        # the workspace's gmax_part now holds a launch's max|g| partials: from the next step on a
+        # Snake last layer may run fused with the head, its backward scale taken from them
+        # (include/siren_hip.h siren_batch.head_scale_prev)
+        for b in self.batches:
+            b.head_scale_prev = 1
 
     def _launch_update(self):
         check(self.lib.siren_apply_update(

@@ -148,12 +148,21 @@ class _KanFunction(torch.autograd.Function):
         b.coords, b.target, b.out, b.g, b.ws = ptr(xs), 0, ptr(out), ptr(g), ptr(ws)
         check(lib.siren_kan_forward(ctypes.byref(net), ctypes.byref(b), torch.cuda.current_stream(dev).cuda_stream),
               "siren_kan_forward")
+        # the input and parameters go through save_for_backward so that torch's version counter
+        # catches an in-place change between forward and backward (the workspace holds state
+        # computed from them, e.g. the combined spline_w * scaler weights); the rest is non-tensor
+        # state and the workspace
+        ctx.save_for_backward(x, *params)
         ctx.keep = (net, b, ws, xs, g, p, x.shape, [t.shape for t in params])
         return out.reshape(*x.shape[:-1], widths[-1])
 
     @staticmethod
     def backward(ctx, grad_out):
         lib = _lib.load()
+        _ = ctx.saved_tensors  # raises if x or a parameter was modified in place since the forward
+        if ctx.keep is None:
+            raise RuntimeError("KAN HIP backward: the forward's workspace is consumed by the first backward; "
+                               "run the forward again instead of backward(retain_graph=True) twice")
         net, b, ws, xs, g, p, xshape, shapes = ctx.keep
         dev = xs.device
         g.copy_(grad_out.reshape(g.shape).float())

@@ -369,7 +369,7 @@ def main():
     ap.add_argument("--only-multiwave", action="store_true",
                     help="write only the MultiWaveformFitting and reference-checkpoint fixtures")
     args = ap.parse_args()
-    torch.set_num_threads(os.cpu_count() or 1)
+    torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", 0)) or os.cpu_count() or 1)
     ref_models, ref_utils = import_reference()
     if args.clip:
         _, target = ref_utils.WaveformFitting(os.path.join(REF, "gt_bach.wav"), duration=args.clip, decimation=1)[0]

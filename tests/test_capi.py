@@ -44,7 +44,7 @@ def test_struct_layouts_match(lib):
 
 
 def test_host_only_helpers(lib):
-    assert lib.siren_abi_version() == 10
+    assert lib.siren_abi_version() == 11
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256
@@ -82,6 +82,13 @@ def test_validation_without_device(lib):
                                     1, 1, None) == 1001
     assert lib.siren_head_fused_fwd(1, 1, 1, f(30), 1024, 256, 1, 1, f(0), 1, 1024, 1024.0, 2, 1, 1, 1, 1, 1, 1,
                                     1, 1, None) == 1003
+    # ... and for a last layer of any kind: a Snake without its a, an unknown activation
+    A = lambda act, a, rows=1024, lm=0: lib.siren_head_fused_fwd_act(  # noqa: E731
+        1, 1, 1, act, f(30), a, rows, 256, 1, 1, f(0), 1, rows, float(rows), lm, 1, 1, 1, 1, 1, 1, None, 1, 1, None)
+    assert A(1, None) == 1002
+    assert A(3, 1) == 1003
+    assert A(2, None, rows=1152) == 1001
+    assert A(2, None, lm=2) == 1003
     assert lib.siren_grad_scale_bound(None, 10, None, 1, 1, 256, 10.0, f(0), 0, f(30), 1, None) == 1002
     assert lib.siren_grad_scale_bound(1, -1, 1, 1, 1, 256, 10.0, f(0), 0, f(30), 1, None) == 1001
     assert lib.siren_grad_scale_bound(1, 10, 1, 1, 1, 256, 10.0, f(0), 3, f(30), 1, None) == 1003

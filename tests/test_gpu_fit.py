@@ -126,6 +126,9 @@ def test_fit_quality_vs_reference_over_seeds(dev):
           f"\nper seed GPU  best {np.round(best_gpu, 2).tolist()} final {np.round(fin_gpu, 2).tolist()}"
           f"\nper seed ref  best {np.round(best_ref, 2).tolist()} final {np.round(fin_ref, 2).tolist()}")
     assert abs(med(best_gpu) - med(best_ref)) < BOUND_3X256
+    # ... and inside this run's own envelope: the reference's median moved by its summation order
+    # alone (fp32 torch on this GPU), plus north_star's 0.1 dB (the fixed bound is the cap)
+    assert abs(med(best_gpu) - med(best_ref)) < 0.1 + abs(med(best_t32) - med(best_ref))
     assert med(fin_gpu) >= med(fin_ref) - 15.0
     assert abs(med(tail_gpu) - med(tail_ref)) < 11.0
 
@@ -168,6 +171,8 @@ def test_fit_quality_headline_model_over_seeds(dev):
           f"lr drops GPU {drops_gpu} reference {drops_ref}")
     assert drops_ref > 0 and drops_gpu > 0
     assert abs(med(best_gpu) - med(best_ref)) < BOUND_5X1024_CHAOTIC
+    # the per-run envelope as well (see test_fit_quality_vs_reference_over_seeds)
+    assert abs(med(best_gpu) - med(best_ref)) < 0.1 + abs(med(best_t32) - med(best_ref))
 
 
 def test_fit_headline_model_stable_regime_per_seed(dev):

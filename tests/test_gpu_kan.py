@@ -159,6 +159,26 @@ def test_kan_autograd_vs_oracle(dev):
         assert rel < 1e-4, (k, rel)
 
 
+def test_kan_autograd_guards(dev):
+    """_KanFunction keeps its inputs under torch's version counter (an in-place parameter change
+    between forward and backward raises instead of giving silently wrong gradients), and a second
+    backward through a retained graph raises a clear RuntimeError."""
+    m = _kan([1, 16, 16, 1]).to(dev)
+    t, y = _data(600)
+    x = torch.from_numpy(t).to(dev).reshape(1, -1, 1)
+    yt = torch.from_numpy(y).to(dev).reshape(1, -1, 1)
+    loss = torch.nn.MSELoss()(m(x), yt)
+    with torch.no_grad():
+        m.layers[0].base_weight.add_(1.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        loss.backward()
+    m.zero_grad()
+    loss = torch.nn.MSELoss()(m(x), yt)
+    loss.backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="run the forward again"):
+        loss.backward()
+
+
 def test_kan_torch_optim_loop_matches_engine(dev):
     """A hand-written torch.optim.Adam loop on the differentiable KAN follows the fused KanEngine
     fit (same gradients, torch's Adam vs the device Adam kernel) and the oracle's Adam on the

@@ -113,18 +113,23 @@ _PK_NEW = """typedef float f32x2 __attribute__((ext_vector_type(2)));
 # fused head (NT_FWD_HB) cost split: no hand-off (each block uses its own partial for all column
 # tiles: WRONG g, timing only)
 _HB_WAIT_OLD = """            while ((u = __hip_atomic_load(hpu + (size_t)jt * p.M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
-                   kHeadPending)
-              __builtin_amdgcn_s_sleep(1);"""
-_HB_WAIT_NEW = """            u = __float_as_uint(own) + jt;"""
+                   kHeadPending) {"""
+_HB_WAIT_NEW = """            u = __float_as_uint(own) + jt;
+            while (polls == 12345) {"""
+# no hand-off at all: the partials are neither published nor awaited (WRONG g, timing and write
+# attribution only: head_part receives no stores)
+_HB_PUB_OLD = """        __hip_atomic_store(hpu + (size_t)tn * p.M + m, own == own ? __float_as_uint(own) : 0x7fc00000u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);"""
+_HB_PUB_NEW = """        if (own == 12345.0f) hpu[(size_t)tn * p.M + m] = __float_as_uint(own);"""
 
 # phase 2 without its dZ stores (the column partials still computed): WRONG dZ, timing only
 _HB_ST_OLD = """          st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));"""
 _HB_ST_NEW = """          if (gm[j] == 12345.0f) st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));"""
 # no phase 2 at all (only phase 1 and the hand-off): timing only
 _HB_PH2_OLD = """      for (int pp = 0; pp < SN / 2; ++pp) {
-        float cs[2][2][4];  // [db_L, dw_head][subtile h][column r]"""
+        float cs[NQ][2][4];  // [db_L, dw_head, da_L][subtile h][column r]"""
 _HB_PH2_NEW = """      for (int pp = 0; pp < (p.n_valid == -7 ? SN / 2 : 0); ++pp) {
-        float cs[2][2][4];  // [db_L, dw_head][subtile h][column r]"""
+        float cs[NQ][2][4];  // [db_L, dw_head, da_L][subtile h][column r]"""
 
 # forward stores folded onto the first 512 rows of Y / C (1 MB each: L2-resident, no HBM write-back):
 # WRONG outputs, timing only -- prices the forward's 4.3 GB of output writes against HBM
@@ -245,6 +250,9 @@ VARIANTS = {
     "fl_nt": {"gemm_nt.hip": [(_ST16, _st16_asm("nt")), (_FL_OLD, _FL_NEW)]},  # whole-line non-temporal
     "st_l2": {"gemm_nt.hip": [(_L2ST_OLD, _L2ST_NEW)]},
     "hb_nowait": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW)]},
+    "hb_nopub": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW), (_HB_PUB_OLD, _HB_PUB_NEW)]},
+    "hb_nopub_nostore": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW), (_HB_PUB_OLD, _HB_PUB_NEW),
+                                         (_HB_ST_OLD, _HB_ST_NEW)]},
     "hb_nostore": {"gemm_nt.hip": [(_HB_ST_OLD, _HB_ST_NEW)]},
     "hb_noph2": {"gemm_nt.hip": [(_HB_PH2_OLD, _HB_PH2_NEW)]},
     "pkfma": {"gemm_nt.hip": [(_PK_OLD, _PK_NEW)]},
