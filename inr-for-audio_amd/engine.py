@@ -62,17 +62,30 @@ def net_spec(model) -> NetSpec:
 
 class ParamLayout:
     """Offsets of every parameter (named_parameters order == state_dict order == the
-    order torch.optim.Adam indexes its state) inside the flat fp32 vectors."""
+    order torch.optim.Adam indexes its state) inside the flat fp32 vectors.
 
-    def __init__(self, model):
+    `pad` ({parameter index: (stored shape, fill value)}) stores a parameter zero-padded to the
+    width the kernels run at (a hidden width that is not 128/256/512/1024 runs as the next one
+    of those; models.SirenWithSnakeTanh.hip_padding): `view` is the stored (padded) tensor the
+    C-ABI binds, `true_view` the model's own [:h, ...] block of it.  Pad entries start at their
+    fill value (0, or 1 for a Snake a) and their gradients are exactly zero, so Adam never moves
+    them and the padded network computes the unpadded one's function and gradients."""
+
+    def __init__(self, model, pad: dict | None = None):
+        pad = pad or {}
         self.names, self.shapes, self.offsets, self.numels = [], [], [], []
+        self.true_shapes, self.fills = [], []
         off = 0
-        for name, p in model.named_parameters():
+        for i, (name, p) in enumerate(model.named_parameters()):
+            shp, fill = pad.get(i, (tuple(p.shape), 0.0))
+            assert len(shp) == p.dim() and all(a >= b for a, b in zip(shp, p.shape)), (name, shp)
             self.names.append(name)
-            self.shapes.append(tuple(p.shape))
+            self.shapes.append(tuple(shp))
+            self.true_shapes.append(tuple(p.shape))
+            self.fills.append(float(fill))
             self.offsets.append(off)
-            self.numels.append(p.numel())
-            off = round_up(off + p.numel(), SEG_ALIGN)
+            self.numels.append(math.prod(shp))
+            off = round_up(off + self.numels[-1], SEG_ALIGN)
         self.n_params = off                   # Adam runs over [0, n_params)
         self.sse_offset = off                 # summed squared error rides the all-reduce
         self.flat_len = off + SEG_ALIGN
@@ -80,6 +93,19 @@ class ParamLayout:
     def view(self, flat: torch.Tensor, i: int) -> torch.Tensor:
         o = self.offsets[i]
         return flat[o:o + self.numels[i]].view(self.shapes[i])
+
+    def true_view(self, flat: torch.Tensor, i: int) -> torch.Tensor:
+        v = self.view(flat, i)
+        if self.shapes[i] == self.true_shapes[i]:
+            return v
+        return v[tuple(slice(0, d) for d in self.true_shapes[i])]
+
+    def fill_pads(self, flat: torch.Tensor) -> None:
+        """Every padded parameter's stored tensor to its fill value (the model block is then
+        copied over it)."""
+        for i, f in enumerate(self.fills):
+            if self.shapes[i] != self.true_shapes[i]:
+                self.view(flat, i).fill_(f)
 
 
 class Workspace:
@@ -245,19 +271,21 @@ class SirenEngine:
             raise RuntimeError("SirenEngine runs on the GPU only (HIP kernels; no CPU fallback)")
         self.model = model
         self.spec = spec = net_spec(model)
-        self.layout = lay = ParamLayout(model)
+        self.layout = lay = ParamLayout(model, model.hip_padding())
         dev = self.device
 
-        # flat fp32 parameter storage; module parameters become views into it
+        # flat fp32 parameter storage; module parameters become views into it (the model's own
+        # blocks of the padded tensors when the hidden width is padded)
         self.params = torch.zeros(lay.flat_len, dtype=torch.float32, device=dev)
         with torch.no_grad():
+            lay.fill_pads(self.params)
             for i, (_, p) in enumerate(model.named_parameters()):
-                lay.view(self.params, i).copy_(p.detach().to(dev, torch.float32))
+                lay.true_view(self.params, i).copy_(p.detach().to(dev, torch.float32))
         d = _dist()
         if d is not None:
             d.broadcast(self.params, src=0)
         for i, (_, p) in enumerate(model.named_parameters()):
-            p.data = lay.view(self.params, i)
+            p.data = lay.true_view(self.params, i)
         self.grads = torch.zeros_like(self.params)
         self.exp_avg = torch.zeros_like(self.params)
         self.exp_avg_sq = torch.zeros_like(self.params)
@@ -447,7 +475,8 @@ class SirenEngine:
         return float(self.loss_hist[k].item()) if k >= 0 else float("nan")
 
     def grad_views(self):
-        return [self.layout.view(self.grads, i) for i in range(len(self.layout.names))]
+        """The gradient of every parameter, in the model's own shapes (named_parameters order)."""
+        return [self.layout.true_view(self.grads, i) for i in range(len(self.layout.names))]
 
     @torch.no_grad()
     def infer(self, coords: torch.Tensor, chunk: int | None = None) -> torch.Tensor:
@@ -466,8 +495,8 @@ class SirenEngine:
         for i in range(len(self.layout.names)):
             state[i] = {
                 "step": torch.tensor(float(st.step)),
-                "exp_avg": self.layout.view(self.exp_avg, i).detach().cpu().clone(),
-                "exp_avg_sq": self.layout.view(self.exp_avg_sq, i).detach().cpu().clone(),
+                "exp_avg": self.layout.true_view(self.exp_avg, i).detach().cpu().clone(),
+                "exp_avg_sq": self.layout.true_view(self.exp_avg_sq, i).detach().cpu().clone(),
             }
         group = {"lr": float(st.lr), "betas": (st.beta1, st.beta2), "eps": st.eps, "weight_decay": 0,
                  "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
@@ -483,8 +512,9 @@ class SirenEngine:
                 s = sd["state"].get(i)
                 if s is None:
                     continue
-                self.layout.view(self.exp_avg, i).copy_(s["exp_avg"].reshape(self.layout.shapes[i]))
-                self.layout.view(self.exp_avg_sq, i).copy_(s["exp_avg_sq"].reshape(self.layout.shapes[i]))
+                shp = self.layout.true_shapes[i]
+                self.layout.true_view(self.exp_avg, i).copy_(s["exp_avg"].reshape(shp))
+                self.layout.true_view(self.exp_avg_sq, i).copy_(s["exp_avg_sq"].reshape(shp))
                 step = float(s["step"])
             st = self.opt_state()
             st.step = step

@@ -135,9 +135,7 @@ class SirenWithSnakeTanh(nn.Module):
                                       "num_tanh >= 1)")
         if self.in_features not in (1, 2):
             raise NotImplementedError("HIP path: in_features must be 1 or 2")
-        H = self.hidden_features
-        if H % 128 or H > 1024 or 256 % (H // 4):
-            raise NotImplementedError(f"HIP path: hidden_features must be 128/256/512/1024, got {H}")
+        H = self.hip_width()
         if n_inner > _lib.MAX_INNER:
             raise NotImplementedError(f"HIP path: num_sine + num_snake + num_tanh <= {_lib.MAX_INNER}")
         acts = (_lib.ACT_SINE,) * self.num_sine + (_lib.ACT_SNAKE,) * self.num_snake + \
@@ -145,6 +143,47 @@ class SirenWithSnakeTanh(nn.Module):
         return NetSpec(self.in_features, H, n_inner, float(self.first_omega_0),
                        float(self.hidden_omega_0), acts, bool(self.first_linear),
                        0.0 if self.last_linear else float(self.hidden_omega_0))
+
+    def hip_width(self) -> int:
+        """The hidden width the kernels run at: hidden_features itself when it is 128, 256, 512
+        or 1024, else the next of those -- the network is zero-padded to it (hip_padding), which
+        computes the unpadded network's function and gradients exactly (padded units have zero
+        weights in and out: their outputs are 0 and every gradient that touches them is 0)."""
+        H = int(self.hidden_features)
+        for w in (128, 256, 512, 1024):
+            if H <= w:
+                return w
+        raise NotImplementedError(f"HIP path: hidden_features <= 1024 (the NT epilogue's per-column LDS "
+                                  f"vectors), got {H}")
+
+    def hip_padding(self) -> dict:
+        """{parameter index: (stored shape, fill)} for engine.ParamLayout when hidden_features is
+        padded to hip_width(): the hidden axes of W0, b0, every W_i (both), b_i, Snake a (filled
+        with 1, so that the padded units' sin^2(a z)/a stays finite), the head weight."""
+        H, Hp = int(self.hidden_features), self.hip_width()
+        if H == Hp:
+            return {}
+        ix = self.param_index()
+        params = [p for _, p in self.named_parameters()]
+        pad = {}
+
+        def put(k, shape, fill=0.0):
+            if params[k].dim() != len(shape):
+                raise NotImplementedError(f"HIP path: cannot pad a parameter of shape {tuple(params[k].shape)} "
+                                          f"to width {Hp}")
+            pad[k] = (shape, fill)
+
+        put(ix["W0"], (Hp, self.in_features))
+        put(ix["b0"], (Hp,))
+        if ix["a0"] is not None:
+            put(ix["a0"], (Hp,), 1.0)
+        for i in range(len(ix["W"])):
+            put(ix["W"][i], (Hp, Hp))
+            put(ix["b"][i], (Hp,))
+            if ix["a"][i] is not None:
+                put(ix["a"][i], (Hp,), 1.0)
+        put(ix["wh"], (1, Hp))
+        return pad
 
     def param_index(self):
         """Positions in named_parameters() order (== state_dict order == Adam's state index)
@@ -221,8 +260,8 @@ class SirenWithSnakeTanh(nn.Module):
         spec = self.hip_spec()
         lead = coords.shape[:-1]
         params = [p for _, p in self.named_parameters()]
-        out = _SirenFunction.apply((spec, self.param_index()), coords.reshape(-1, spec.in_dim).detach(),
-                                   *params)
+        ix = dict(self.param_index(), pad=self.hip_padding())
+        out = _SirenFunction.apply((spec, ix), coords.reshape(-1, spec.in_dim).detach(), *params)
         return out.reshape(*lead, 1)
 
 
@@ -238,7 +277,17 @@ class _SirenFunction(torch.autograd.Function):
         L, H = spec.n_inner, spec.hidden
         n = coords.shape[0]
         rows = round_up(max(n, 1), ROW_TILE)
-        p = [t.detach().contiguous().float() for t in params]
+        # the kernels' width: padded copies when hidden_features is not 128/256/512/1024
+        pad = ix.get("pad", {})
+        p = []
+        for k, t in enumerate(params):
+            t = t.detach().float()
+            if k in pad:
+                shp, fill = pad[k]
+                full = torch.full(shp, fill, dtype=torch.float32, device=dev)
+                full[tuple(slice(0, d) for d in t.shape)] = t
+                t = full
+            p.append(t.contiguous())
         W = [p[k] for k in ix["W"]]
         Wh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
         WTh = [torch.empty(H, H, dtype=STORE16, device=dev) for _ in range(L)]
@@ -253,14 +302,14 @@ class _SirenFunction(torch.autograd.Function):
         tgt = torch.zeros(rows, dtype=torch.float32, device=dev)
         b = ws.batch(xc, tgt, n, float(n))
         _lib.check(lib.siren_forward(ctypes.byref(net), ctypes.byref(b), s), "siren_forward")
-        ctx.keep = (spec, ix, net, ws, xc, tgt, p, Wh, WTh, n, [t.shape for t in params])
+        ctx.keep = (spec, ix, net, ws, xc, tgt, p, Wh, WTh, n, [t.shape for t in p], [t.shape for t in params])
         return ws.out[:n].clone()
 
     @staticmethod
     def backward(ctx, grad_out):
         from .engine import SEG_ALIGN, round_up
         from ._lib import SirenGrads, ptr
-        spec, ix, net, ws, xc, tgt, p, Wh, WTh, n, shapes = ctx.keep
+        spec, ix, net, ws, xc, tgt, p, Wh, WTh, n, shapes, true_shapes = ctx.keep
         lib = _lib.load()
         dev = xc.device
         L = spec.n_inner
@@ -287,7 +336,9 @@ class _SirenFunction(torch.autograd.Function):
         _lib.check(lib.siren_backward(ctypes.byref(net), ctypes.byref(gs), ctypes.byref(b), s),
                    "siren_backward")
         ctx.keep = None
-        return (None, None, *views)
+        # the model's own blocks of the (possibly padded) gradients
+        grads = [v if v.shape == ts else v[tuple(slice(0, d) for d in ts)] for v, ts in zip(views, true_shapes)]
+        return (None, None, *grads)
 
 
 # ---- unfused fp32 layers (layer_fp32.hip): the module API outside the fused step ----------

@@ -212,3 +212,70 @@ def test_tiny_and_ragged_inputs(dev, n):
     kref = orc.kan_backward(ksd, xs, orc.mse_grad(kout, y.numpy()), 3)
     for k, r in kref.items():
         assert _rel(kgot[k].reshape(r.shape), r) < 1e-4, k
+
+
+@pytest.mark.parametrize("H,cfg,n,fl,ll", [
+    (100, (2, 0, 0), 1500, False, True),     # a width the reference accepts (models.py:310), padded to 128
+    (200, (1, 1, 0), 1500, True, False),     # Linear + Snake first, Snake a padded with 1, final SineLayer
+    (384, (1, 0, 1), 1024, False, True),     # padded to 512, Tanh last
+])
+def test_padded_hidden_width_vs_oracle(dev, H, cfg, n, fl, ll):
+    """hidden_features that is not 128/256/512/1024 runs zero-padded to the next kernel width: the
+    step's gradients in the model's own shapes equal the oracle's for the unpadded network, every
+    pad entry's gradient is exactly 0, and after three Adam steps the pads still hold their fill
+    (0, or 1 for a Snake a)."""
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(3)
+    model = SirenWithSnakeTanh(1, 1, H, *cfg, first_linear=fl, last_linear=ll, first_omega_0=1000.0,
+                               hidden_omega_0=30.0, a_initial=0.5)
+    sd0 = _sd(model)
+    t, y = _signal(n)
+    eng = SirenEngine(model, t, y, lr=1e-3, device=dev)
+    assert eng.spec.hidden == model.hip_width() > H
+    eng.step()
+    torch.cuda.synchronize()
+    got = {k: v.detach().cpu().numpy() for k, v in zip(eng.layout.names, eng.grad_views())}
+    p = orc.Params.from_state_dict(sd0, *cfg, fl, ll)
+    out, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
+    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), 1000.0, 30.0, half=True)
+    assert set(ref) == set(got)
+    check_grads(f"padded_width_step[{H}x{cfg}x{fl}x{ll}]", got, ref)
+    lay = eng.layout
+    for _ in range(2):
+        eng.step()
+    torch.cuda.synchronize()
+    for i, name in enumerate(lay.names):
+        if lay.shapes[i] == lay.true_shapes[i]:
+            continue
+        mask = torch.ones(lay.shapes[i], dtype=torch.bool, device=dev)
+        mask[tuple(slice(0, d) for d in lay.true_shapes[i])] = False
+        assert bool((lay.view(eng.grads, i)[mask] == 0).all()), name
+        fill = 1.0 if name.endswith(".a") else 0.0
+        assert bool((lay.view(eng.params, i)[mask] == fill).all()), name
+    # the module's parameters are the model-shaped blocks, and the state_dict round-trips
+    assert {k: tuple(v.shape) for k, v in model.state_dict().items()} == {k: v.shape for k, v in sd0.items()}
+    # inference through the padded network = the model's own forward (autograd drop-in, also padded)
+    with torch.no_grad():
+        a = eng.infer(t.to(dev)).cpu()
+        b = model(t.to(dev)).reshape(-1).cpu()
+    assert float((a - b).abs().max()) <= 1e-6 * float(b.abs().max()) + 1e-7
+
+
+def test_padded_width_autograd_dropin(dev):
+    """model(x) / loss.backward() at hidden_features=100: HIP forward and backward through the
+    padded kernels, gradients in the model's shapes vs the oracle."""
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(5)
+    model = SirenWithSnakeTanh(1, 1, 100, 2, 0, 0, first_omega_0=1000.0, hidden_omega_0=30.0)
+    sd0 = _sd(model)
+    t, y = _signal(1200)
+    model = model.to(dev)
+    out = model(t.to(dev))
+    loss = torch.nn.MSELoss()(out, y.to(dev))
+    loss.backward()
+    p = orc.Params.from_state_dict(sd0, 2)
+    ref_out, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
+    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(ref_out, y.numpy()), 1000.0, 30.0, half=True)
+    got = {k: v.grad.detach().cpu().numpy() for k, v in model.named_parameters()}
+    check_grads("padded_width_autograd", got, ref)

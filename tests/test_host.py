@@ -54,11 +54,43 @@ def test_param_layout():
         assert tuple(v.shape) == shp and int(v.reshape(-1)[0]) == lay.offsets[i]
 
 
+@pytest.mark.parametrize("H,cfg,fl,ll,Hp", [
+    (100, (2, 0, 0), False, True, 128), (384, (1, 1, 1), False, True, 512), (200, (0, 2, 0), True, False, 256),
+    (1000, (1, 0, 0), False, True, 1024), (3, (1, 1, 0), False, True, 128)])
+def test_hidden_width_padding(H, cfg, fl, ll, Hp):
+    """Any hidden_features <= 1024 runs zero-padded to the next kernel width (models.py:310 accepts
+    any width): the layout stores the padded tensors, the model's parameters are their [:H] blocks,
+    a Snake a's pad entries are 1 and every other pad entry is 0."""
+    from inr_for_audio_amd.engine import ParamLayout
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(0)
+    m = SirenWithSnakeTanh(1, 1, H, *cfg, first_linear=fl, last_linear=ll, first_omega_0=300.0, a_initial=0.5)
+    assert m.hip_width() == Hp and m.hip_spec().hidden == Hp
+    pad = m.hip_padding()
+    lay = ParamLayout(m, pad)
+    flat = torch.full((lay.flat_len,), 7.0)
+    lay.fill_pads(flat)
+    sd = m.state_dict()
+    for i, (name, p) in enumerate(m.named_parameters()):
+        tv = lay.true_view(flat, i)
+        assert tuple(tv.shape) == tuple(p.shape), name
+        tv.copy_(p.detach())
+        v = lay.view(flat, i)
+        assert all(d in (Hp, 1, m.in_features) for d in v.shape), (name, v.shape)
+        assert torch.equal(lay.true_view(flat, i), sd[name])
+        if i in pad:
+            mask = torch.ones_like(v, dtype=torch.bool)
+            mask[tuple(slice(0, d) for d in p.shape)] = False
+            want = 1.0 if name.endswith(".a") else 0.0
+            assert bool((v[mask] == want).all()), name
+    assert (m.hip_padding() == {}) == (H == Hp)
+
+
 def test_hip_spec_validation():
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     spec = _model(256, 2, 22000.0).hip_spec()
     assert (spec.in_dim, spec.hidden, spec.n_inner, spec.omega0, spec.omega) == (1, 256, 2, 22000.0, 30.0)
-    bad = [dict(hidden_features=384), dict(num_sine=0), dict(in_features=3), dict(out_features=2),
+    bad = [dict(hidden_features=1100), dict(num_sine=0), dict(in_features=3), dict(out_features=2),
            dict(num_sine=10, num_snake=4, num_tanh=3)]
     for kw in bad:
         args = dict(in_features=1, out_features=1, hidden_features=256, num_sine=2, num_snake=0, num_tanh=0)

@@ -238,6 +238,36 @@ _PRIO_OLD2 = """      __builtin_amdgcn_s_setprio(1);
       __builtin_amdgcn_s_setprio(0);"""
 _PRIO_NEW2 = """      mma(sg);"""
 
+# Snake fused last layer: E (dY/da) parked in the dZ_L buffer across the hand-off instead of 64
+# VGPRs (the product's 400 B of spills): phase 1 stores each row piece's E where its dZ_L piece
+# will go, phase 2 loads it back right before overwriting it with dZ_L (the lines stay in L2, so
+# HBM sees the final dZ_L only if they are not evicted in between).  Outputs bit-identical.
+_HBS_EZ_OLD1 = """            hp[j] += sv[0] * hw[i].x + sv[1] * hw[i].y + sv[2] * hw[i].z + sv[3] * hw[i].w;
+          }
+        }
+      }"""
+_HBS_EZ_NEW1 = """            hp[j] += sv[0] * hw[i].x + sv[1] * hw[i].y + sv[2] * hw[i].z + sv[3] * hw[i].w;
+          }
+          if constexpr (SNK)
+            st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32,
+                 swap16_pair(e16[SNK ? 2 * pp : 0][SNK ? j : 0], e16[SNK ? 2 * pp + 1 : 0][SNK ? j : 0]));
+        }
+      }"""
+_HBS_EZ_OLD2 = """          uint2 dzp[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * pp + h;
+            const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);"""
+_HBS_EZ_NEW2 = """          uint2 dzp[2];
+          uint2 eu[2];
+          if constexpr (SNK) unswap16_pair(*(const uint4*)(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32), eu[0], eu[1]);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * pp + h;
+            const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);"""
+_HBS_EZ_OLD3 = """              const h16x4 eh = as_h4(e16[SNK ? i : 0][SNK ? j : 0]);"""
+_HBS_EZ_NEW3 = """              const h16x4 eh = as_h4(eu[h]);"""
+
 VARIANTS = {
     "noprio": {"gemm_pipeline.h": [(_PRIO_OLD1, _PRIO_NEW1), (_PRIO_OLD2, _PRIO_NEW2)]},
     "tnserp": {"gemm_tn.hip": [(_TNORD_OLD, _TNSERP_NEW)]},
@@ -250,6 +280,7 @@ VARIANTS = {
     "fl_nt": {"gemm_nt.hip": [(_ST16, _st16_asm("nt")), (_FL_OLD, _FL_NEW)]},  # whole-line non-temporal
     "st_l2": {"gemm_nt.hip": [(_L2ST_OLD, _L2ST_NEW)]},
     "hb_nowait": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW)]},
+    "hbs_ez": {"gemm_nt.hip": [(_HBS_EZ_OLD1, _HBS_EZ_NEW1), (_HBS_EZ_OLD2, _HBS_EZ_NEW2), (_HBS_EZ_OLD3, _HBS_EZ_NEW3)]},
     "hb_nopub": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW), (_HB_PUB_OLD, _HB_PUB_NEW)]},
     "hb_nopub_nostore": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW), (_HB_PUB_OLD, _HB_PUB_NEW),
                                          (_HB_ST_OLD, _HB_ST_NEW)]},
