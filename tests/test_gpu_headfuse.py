@@ -186,3 +186,34 @@ def test_kernel_vs_unfused_launches(dev, lib, opts, H, R, n_valid, grid):
     for got, ref in ((part1[:, 0].double().sum(0), db2.double().sum(0)), (part1[:, 1].double().sum(0),
                                                                           dw2.double().sum(0))):
         assert float((got - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) + 1e-12
+
+
+def test_fused_head_needs_a_coresident_grid(dev, lib, opts):
+    """The fused last layer's bands wait for each other's head partials, so its grid must be
+    co-resident: a persistent grid larger than the device can hold (forced through
+    SIREN_OPT_NT_GRID) is not fused -- siren_train_step falls back to the unfused launches and
+    computes the same step; siren_head_fused_fwd refuses it with an error instead of launching."""
+    import ctypes
+    opts(OPT_NT_TILE, 256)
+    eng, _, _, _ = _engine(dev, 1024, 2, 65536)   # 1 024 tiles of 256^2
+    ga, oa, gga, ka = _grads(eng, lib)
+    assert ka["head_fwd"] == 1
+    opts(OPT_NT_GRID, 1024)                        # more blocks than CUs x occupancy (1 per CU)
+    gb, ob, ggb, kb = _grads(eng, lib)
+    assert kb["head_fwd"] == 0 and kb["inner_fwd"] == 2
+    assert torch.equal(oa, ob) and torch.equal(gga, ggb)
+    lay = eng.layout
+    for i, k in enumerate(lay.names):
+        assert _rel(lay.view(ga, i), lay.view(gb, i)) < 2e-5, k
+    # the entry point itself: real buffers (a launch, were it to happen, would be well-formed)
+    R, H = 65536, 1024
+    P = lambda t: t.data_ptr()  # noqa: E731
+    z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
+    X, W, dZ = z(R, H, dt=torch.float16), z(H, H, dt=torch.float16), z(R, H, dt=torch.float16)
+    b, wh, bh, y, gs = z(H), z(H), z(1), z(R), torch.tensor([1.0, 1.0], device=dev)
+    hp, out, g, sse, gsum, part = z(H // 256, R), z(R), z(R), z(R // 256), z(R // 256), z(R // 256, 2, H)
+    st = lib.siren_head_fused_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(wh), P(bh), ctypes.c_float(0.0),
+                                  P(y), R, float(R), 0, P(gs), P(hp), P(out), P(g), P(sse), P(gsum), P(dZ), P(part),
+                                  torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert st != 0, "a grid larger than the device holds must not launch the fused kernel"
