@@ -230,12 +230,15 @@ int siren_head_fused_fwd(const uint16_t* X, const uint16_t* Wh, const float* b, 
  * with their derivative in place of the cosine (omega unused) -- dZ, out, g and the partials as
  * siren_inner_fwd_act -> siren_head_loss -> siren_head_bwd compute them at the same gscale;
  * part[rows/256][2][hidden] (db_L, dw_head), Snake part[rows/256][3][hidden] (+ da_L);
- * gmax_part (nullable): [rows/256] max|g| per 256 rows, as siren_head_loss writes it */
+ * gmax_part (nullable): [rows/256] max|g| per 256 rows, as siren_head_loss writes it; E (Snake,
+ * else ignored): fp16 [rows][hidden], receives the layer's dY/da as siren_inner_fwd_act writes it
+ * (the kernel reads it back for the da_L partials) */
 int siren_head_fused_fwd_act(const uint16_t* X, const uint16_t* Wh, const float* b, int32_t act, float omega,
                              const float* a, int32_t rows, int32_t hidden, const float* w_head, const float* b_head,
                              float head_omega, const float* y, int32_t n_valid, double n_total, int32_t loss_mode,
                              const float* gscale, float* head_part, float* out, float* g, float* sse_part,
-                             float* gsum_part, float* gmax_part, uint16_t* dZ, float* part, void* stream);
+                             float* gsum_part, float* gmax_part, uint16_t* dZ, float* part, uint16_t* E,
+                             void* stream);
 /* the fused head's backward scale, fixed before the forward: gscale = {S, 1/S} from a bound of
  * max|g| (MSE: (sum|w_head| + |b_head| + max|y|) 2/n_total, or 1 + max|y| through a final sine of
  * head_omega; L1: 1/n_total; x head_omega) x max|w_head| x act_bound (|dY/dz| bound of the last

@@ -152,7 +152,7 @@ _SIGS = {
                                             ctypes.c_double, _i32, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "siren_head_fused_fwd_act": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_float, _p, _i32, _i32, _p, _p,
                                                 ctypes.c_float, _p, _i32, ctypes.c_double, _i32, _p, _p, _p, _p, _p,
-                                                _p, _p, _p, _p, _p]),
+                                                _p, _p, _p, _p, _p, _p]),
     "siren_grad_scale_bound": (ctypes.c_int, [_p, _i32, _p, _p, _p, _i32, ctypes.c_double, ctypes.c_float, _i32,
                                               ctypes.c_float, _p, _p]),
     "siren_set_option": (ctypes.c_int, [_i32, _i32]),

@@ -533,9 +533,10 @@ int siren_head_fused_fwd_act(const uint16_t* X, const uint16_t* Wh, const float*
                              const float* a, int32_t rows, int32_t hidden, const float* w_head, const float* b_head,
                              float head_omega, const float* y, int32_t n_valid, double n_total, int32_t loss_mode,
                              const float* gscale, float* head_part, float* out, float* g, float* sse_part,
-                             float* gsum_part, float* gmax_part, uint16_t* dZ, float* part, void* stream) {
+                             float* gsum_part, float* gmax_part, uint16_t* dZ, float* part, uint16_t* E,
+                             void* stream) {
   if (!X || !Wh || !b || !w_head || !b_head || !gscale || !head_part || !out || !g || !sse_part || !gsum_part ||
-      !dZ || !part || (n_valid > 0 && !y) || (act == SIREN_ACT_SNAKE && !a))
+      !dZ || !part || (n_valid > 0 && !y) || (act == SIREN_ACT_SNAKE && (!a || !E)))
     return SIREN_ERR_NULL;
   if (!hidden_ok(hidden) || rows <= 0 || rows % 256 || n_valid < 0 || n_valid > rows || !(n_total > 0))
     return SIREN_ERR_SHAPE;
@@ -549,7 +550,7 @@ int siren_head_fused_fwd_act(const uint16_t* X, const uint16_t* Wh, const float*
   p.target = y; p.b_head = b_head; p.out = out; p.g = g; p.sse_part = sse_part; p.gsum_part = gsum_part;
   p.gmax_part = gmax_part;
   p.n_valid = n_valid; p.loss_mode = loss_mode; p.gfac = (float)((loss_mode == 1 ? 1.0 : 2.0) / n_total);
-  p.head_omega = head_omega; p.gscale = gscale; p.dZ = B(dZ); p.colsum_part = part;
+  p.head_omega = head_omega; p.gscale = gscale; p.dZ = B(dZ); p.colsum_part = part; p.E = B(E);
   return (int)gemm_nt(hb_mode(act), true, p, S(stream));
 }
 

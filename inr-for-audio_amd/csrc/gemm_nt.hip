@@ -124,6 +124,20 @@ static_assert(kQueueSet == kTileqInts, "siren_hip.h SIREN_TILEQ_INTS");
 
 constexpr bool nt_is_dx0(int m) { return m == NT_DX0 || m == NT_DX0_SNAKE; }
 
+// tanh for the fp16-stored Tanh epilogues (NT_FWD_TANH, NT_FWD_HB_TANH), branch-free on the hardware
+// exp2 / rcp: sign(x) (1 - e) / (1 + e) with e = exp(-2|x|) (a few fp32 ulp), and the odd Taylor
+// polynomial below |x| < 1/16 where 1 - e would cancel (relative error < 1e-9 there).  ocml's tanhf
+// is branchy and its temporaries made the fused Tanh head spill 184 B per lane; the outputs are
+// stored in fp16 (2^-11), where the two agree to within the parity tests' fp16 bounds.
+__device__ __forceinline__ float tanh_epi(float x) {
+  const float ax = __builtin_fabsf(x);
+  const float e = __builtin_amdgcn_exp2f(ax * -2.8853900817779268f);  // exp(-2|x|) = 2^(-2|x| / ln 2)
+  const float big = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+  const float x2 = ax * ax;
+  const float small = ax * (1.0f + x2 * (-0.33333333f + x2 * (0.13333334f + x2 * -0.053968254f)));
+  return __builtin_copysignf(ax < 0.0625f ? small : big, x);
+}
+
 // NT_FWD_HB: head_part word not yet published by its column tile's block (launch_nt fills it)
 constexpr unsigned kHeadPending = 0xFFFFFFFFu;
 // polls (s_sleep 1 = 64 clocks each, ~1-1.4 s in all) before a hand-off wait gives up; a partner
@@ -331,7 +345,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         hw[i] = *(const float4*)(hw_lds + nq + i * 16);
       }
       float hp[SM];
-      uint2 e16[SNK ? SN : 1][SNK ? SM : 1];  // Snake: fp16 E of the tile
+      uint2 epair[2];  // Snake: fp16 E of one row piece's two column subtiles
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
         hp[j] = 0.f;
@@ -359,17 +373,19 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                 cv[r] = 1.0f + sc2;                // dY/dz
                 ev[r] = (z * sc2 - s2 * ia) * ia;  // dY/da
               }
-              // Y and D packed in place of the accumulators, E beside them (2 VGPRs per 4 elements)
+              // Y and D packed in place of the accumulators; E goes to HBM (p.E, the layer's E
+              // buffer) in 16-B row pieces once both subtiles of the pair have it, and phase 3 reads
+              // it back (held in registers, 64 more VGPRs across the hand-off spilled 400 B per lane)
               const uint2 yv = as_u2(pack4(sv[0], sv[1], sv[2], sv[3])), cw = as_u2(pack4(cv[0], cv[1], cv[2], cv[3]));
               acc[i][j] = __builtin_bit_cast(f32x4, uint4{yv.x, yv.y, cw.x, cw.y});
-              e16[i][j] = as_u2(pack4(ev[0], ev[1], ev[2], ev[3]));
-              asm volatile("" : "+v"(acc[i][j]), "+v"(e16[i][j]));
+              epair[h] = as_u2(pack4(ev[0], ev[1], ev[2], ev[3]));
+              asm volatile("" : "+v"(acc[i][j]));
             } else {
               float cv[4];
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 if constexpr (TNH) {
-                  const float y = tanhf(acc[i][j][r] + bb[r]);
+                  const float y = tanh_epi(acc[i][j][r] + bb[r]);
                   sv[r] = y;
                   cv[r] = 1.0f - y * y;
                 } else {
@@ -386,6 +402,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             }
             hp[j] += sv[0] * hw[i].x + sv[1] * hw[i].y + sv[2] * hw[i].z + sv[3] * hw[i].w;
           }
+          if constexpr (SNK) st16(p.E + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(epair[0], epair[1]));
         }
       }
 #pragma unroll
@@ -472,14 +489,14 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       // Snake, of (g w) E (da_L) over the tile's rows.  Column pairs outermost (the 16-B dZ pieces
       // pair adjacent subtiles), rows inside: each pair's accumulators and column partials die
       // before the next pair's begin
-      constexpr int NQ = SNK ? 3 : 2;
+      constexpr int NQ = 2;  // db_L, dw_head here; a Snake's da_L in phase 3
       const float om = (MODE == NT_FWD_HB) ? p.omega : 1.0f, S = p.gscale[0];
       float gm[SM];
 #pragma unroll
       for (int j = 0; j < SM; ++j) gm[j] = g_lds[wm * TM + j * 16 + (lane & 15)];
 #pragma unroll
       for (int pp = 0; pp < SN / 2; ++pp) {
-        float cs[NQ][2][4];  // [db_L, dw_head, da_L][subtile h][column r]
+        float cs[NQ][2][4];  // [db_L, dw_head][subtile h][column r]
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
 #pragma unroll
@@ -494,7 +511,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             const int i = 2 * pp + h;
             const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);
             const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-            float cf[4], yf[4], ef[4];
+            float cf[4], yf[4];
             const uint4 pk = __builtin_bit_cast(uint4, acc[i][j]);
             const h16x4 yh = as_h4(uint2{pk.x, pk.y}), ch = as_h4(uint2{pk.z, pk.w});
 #pragma unroll
@@ -502,18 +519,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               yf[r] = (float)yh[r];
               cf[r] = (float)ch[r];
             }
-            if constexpr (SNK) {
-              const h16x4 eh = as_h4(e16[SNK ? i : 0][SNK ? j : 0]);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) ef[r] = (float)eh[r];
-            }
             float d[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float dz = ((gm[j] * wv[r]) * cf[r]) * om;
               cs[0][h][r] += dz;
               cs[1][h][r] += gm[j] * yf[r];
-              if constexpr (SNK) cs[2][h][r] += (gm[j] * wv[r]) * ef[r];
               d[r] = dz * S;
             }
             dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
@@ -532,14 +543,54 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                   float4{v[0], v[1], v[2], v[3]};
           }
       }
+      if constexpr (SNK) {
+        // ---- phase 3 (Snake): da_L partials, sum over the tile's rows of (g w) E with E read back
+        // from where phase 1 stored it (L2: written a hand-off earlier).  Every accumulator is dead
+        // by now, so a column pair's 8 row pieces are loaded in one batch (one wait, which also
+        // drains the dZ stores ahead of it in the in-order vmcnt)
+#pragma unroll
+        for (int pp = 0; pp < SN / 2; ++pp) {
+          uint4 eq[SM];
+#pragma unroll
+          for (int j = 0; j < SM; ++j) eq[j] = *(const uint4*)(p.E + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
+          float da[2][4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) da[h][r] = 0.f;
+#pragma unroll
+          for (int j = 0; j < SM; ++j) {
+            uint2 eu[2];
+            unswap16_pair(eq[j], eu[0], eu[1]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const float4 w4 = *(const float4*)(hw_lds + nq + (2 * pp + h) * 16);
+              const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+              const h16x4 eh = as_h4(eu[h]);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) da[h][r] += (gm[j] * wv[r]) * (float)eh[r];
+            }
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = row16_sum(da[h][r]);
+            if ((lane & 15) == 0)
+              *(float4*)(red + (2 * Cfg::WM + wm) * BN + wn * TN + (2 * pp + h) * 16 + 4 * (lane >> 4)) =
+                  float4{v[0], v[1], v[2], v[3]};
+          }
+        }
+      }
       lds_barrier();
       if (tid < BN) {
+        constexpr int NP = SNK ? 3 : 2;  // partial rows: db_L, dw_head (, da_L)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
+        for (int q = 0; q < NP; ++q) {
           float sum = 0.f;
 #pragma unroll
           for (int w = 0; w < Cfg::WM; ++w) sum += red[(q * Cfg::WM + w) * BN + tid];
-          p.colsum_part[((size_t)tm * NQ + q) * N + n0 + tid] = sum;
+          p.colsum_part[((size_t)tm * NP + q) * N + n0 + tid] = sum;
         }
       }
     } else if constexpr (nt_is_fwd(MODE)) {
@@ -598,7 +649,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             } else {  // NT_FWD_TANH
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const float y = tanhf(acc[i][j][r] + bb[r]);
+                const float y = tanh_epi(acc[i][j][r] + bb[r]);
                 s[r] = y;
                 c[r] = 1.0f - y * y;
               }
@@ -1095,7 +1146,7 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (nt_is_hb(mode)) {
     if (!head || p.tile != 256 || !gemm_nt_head_fusable(p.M, p.N, s, mode)) return hipErrorInvalidValue;
     if (!p.head_w || !p.head_part || !p.gscale || !p.dZ || !p.colsum_part || !p.b_head || !p.out || !p.g ||
-        !p.sse_part || !p.gsum_part || (p.n_valid > 0 && !p.target) || (mode == NT_FWD_HB_SNAKE && !p.act_a))
+        !p.sse_part || !p.gsum_part || (p.n_valid > 0 && !p.target) || (mode == NT_FWD_HB_SNAKE && (!p.act_a || !p.E)))
       return hipErrorInvalidValue;
     if (mode == NT_FWD_HB_SNAKE) return launch_nt<NtLargePP, NT_FWD_HB_SNAKE, true>(p, s, true);
     if (mode == NT_FWD_HB_TANH) return launch_nt<NtLargePP, NT_FWD_HB_TANH, true>(p, s, true);

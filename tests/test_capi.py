@@ -83,9 +83,10 @@ def test_validation_without_device(lib):
     assert lib.siren_head_fused_fwd(1, 1, 1, f(30), 1024, 256, 1, 1, f(0), 1, 1024, 1024.0, 2, 1, 1, 1, 1, 1, 1,
                                     1, 1, None) == 1003
     # ... and for a last layer of any kind: a Snake without its a, an unknown activation
-    A = lambda act, a, rows=1024, lm=0: lib.siren_head_fused_fwd_act(  # noqa: E731
-        1, 1, 1, act, f(30), a, rows, 256, 1, 1, f(0), 1, rows, float(rows), lm, 1, 1, 1, 1, 1, 1, None, 1, 1, None)
+    A = lambda act, a, rows=1024, lm=0, e=1: lib.siren_head_fused_fwd_act(  # noqa: E731
+        1, 1, 1, act, f(30), a, rows, 256, 1, 1, f(0), 1, rows, float(rows), lm, 1, 1, 1, 1, 1, 1, None, 1, 1, e, None)
     assert A(1, None) == 1002
+    assert A(1, 1, e=None) == 1002                                         # a Snake needs its E buffer
     assert A(3, 1) == 1003
     assert A(2, None, rows=1152) == 1001
     assert A(2, None, lm=2) == 1003

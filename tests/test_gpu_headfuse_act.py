@@ -68,11 +68,11 @@ def test_kernel_act_vs_unfused_launches(dev, lib, opts, act, H, R, n_valid, grid
     gs = torch.tensor([2.0 ** 9, 2.0 ** -9], device=dev)
     nq = 3 if act == SNAKE else 2
     e = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
-    hp1, out1, g1, dZ1 = e(H // 256, R), e(R), e(R), e(R, H, dt=f16)
+    hp1, out1, g1, dZ1, E1 = e(H // 256, R), e(R), e(R), e(R, H, dt=f16), e(R, H, dt=f16)
     sse1, gsum1, gmax1, part1 = e(R // 256), e(R // 256), e(R // 256), e(R // 256, nq, H)
     st = lib.siren_head_fused_fwd_act(P(X), P(W), P(b), act, ctypes.c_float(30.0), P(a), R, H, P(wh), P(bh),
                                       ctypes.c_float(0.0), P(y), n_valid, float(n_valid), 0, P(gs), P(hp1),
-                                      P(out1), P(g1), P(sse1), P(gsum1), P(gmax1), P(dZ1), P(part1), s)
+                                      P(out1), P(g1), P(sse1), P(gsum1), P(gmax1), P(dZ1), P(part1), P(E1), s)
     assert st == 0, lib.siren_status_string(st)
     Y, C, E, hp2 = e(R, H, dt=f16), e(R, H, dt=f16), e(R, H, dt=f16), e(H // 256, R)
     out2, g2, sse2, gsum2, gmax2, dZ2 = e(R), e(R), e(R // 256), e(R // 256), e(R // 256), e(R, H, dt=f16)
@@ -90,6 +90,8 @@ def test_kernel_act_vs_unfused_launches(dev, lib, opts, act, H, R, n_valid, grid
     assert torch.equal(out1, out2) and torch.equal(g1, g2)
     assert torch.equal(sse1, sse2) and torch.equal(gsum1, gsum2) and torch.equal(gmax1, gmax2)
     assert torch.equal(dZ1, dZ2)
+    if snake:  # the fused kernel leaves the layer's dY/da where the unfused forward writes it
+        assert torch.equal(E1, E)
     pairs = [(part1[:, 0], db2), (part1[:, 1], dw2)] + ([(part1[:, 2], da2)] if snake else [])
     for got, ref in pairs:
         got, ref = got.double().sum(0), ref.double().sum(0)

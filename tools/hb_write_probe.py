@@ -56,6 +56,7 @@ def main():
     hp, out, gg = torch.zeros(H // 256, R, device=dev), torch.zeros(R, device=dev), torch.zeros(R, device=dev)
     sse, gsum, gmax = (torch.zeros(R // 256, device=dev) for _ in range(3))
     dZ = torch.zeros(R, H, dtype=f16, device=dev)
+    E = torch.zeros(R, H, dtype=f16, device=dev)
     part = torch.zeros(R // 256, 3, H, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     order = []
@@ -63,7 +64,8 @@ def main():
         for _ in range(args.reps):
             _lib.check(lib.siren_head_fused_fwd_act(P(X), P(W), P(b), args.act, ctypes.c_float(30.0), P(a), R, H, P(hw),
                                                     P(bh), ctypes.c_float(0.0), P(y), R, float(R), 0, P(gs), P(hp),
-                                                    P(out), P(gg), P(sse), P(gsum), P(gmax), P(dZ), P(part), s),
+                                                    P(out), P(gg), P(sse), P(gsum), P(gmax), P(dZ), P(part), P(E),
+                                                    s),
                        nm)
             order.append(nm)
         torch.cuda.synchronize()

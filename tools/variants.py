@@ -268,6 +268,10 @@ _HBS_EZ_NEW2 = """          uint2 dzp[2];
 _HBS_EZ_OLD3 = """              const h16x4 eh = as_h4(e16[SNK ? i : 0][SNK ? j : 0]);"""
 _HBS_EZ_NEW3 = """              const h16x4 eh = as_h4(eu[h]);"""
 
+# fused last layer, phase 2 rows outermost: both 16-B halves of a dZ_L row segment stored back to back
+_HB_JO_OLD = '#pragma unroll\n      for (int pp = 0; pp < SN / 2; ++pp) {\n        float cs[NQ][2][4];  // [db_L, dw_head][subtile h][column r]\n#pragma unroll\n        for (int q = 0; q < NQ; ++q)\n#pragma unroll\n          for (int h = 0; h < 2; ++h)\n#pragma unroll\n            for (int r = 0; r < 4; ++r) cs[q][h][r] = 0.f;\n#pragma unroll\n        for (int j = 0; j < SM; ++j) {\n          uint2 dzp[2];\n#pragma unroll\n          for (int h = 0; h < 2; ++h) {\n            const int i = 2 * pp + h;\n            const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);\n            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};\n            float cf[4], yf[4];\n            const uint4 pk = __builtin_bit_cast(uint4, acc[i][j]);\n            const h16x4 yh = as_h4(uint2{pk.x, pk.y}), ch = as_h4(uint2{pk.z, pk.w});\n#pragma unroll\n            for (int r = 0; r < 4; ++r) {\n              yf[r] = (float)yh[r];\n              cf[r] = (float)ch[r];\n            }\n            float d[4];\n#pragma unroll\n            for (int r = 0; r < 4; ++r) {\n              const float dz = ((gm[j] * wv[r]) * cf[r]) * om;\n              cs[0][h][r] += dz;\n              cs[1][h][r] += gm[j] * yf[r];\n              d[r] = dz * S;\n            }\n            dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));\n          }\n          st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));\n        }\n#pragma unroll\n        for (int q = 0; q < NQ; ++q)\n#pragma unroll\n          for (int h = 0; h < 2; ++h) {\n            float v[4];\n#pragma unroll\n            for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[q][h][r]);\n            if ((lane & 15) == 0)\n              *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + (2 * pp + h) * 16 + 4 * (lane >> 4)) =\n                  float4{v[0], v[1], v[2], v[3]};\n          }\n      }\n'
+_HB_JO_NEW = "      // rows outermost, both column pairs of a row piece back to back: each 128-B row segment of\n      // dZ_L is then written whole by two consecutive stores (column pairs outermost wrote each\n      // line's halves a pass apart: the HBM writes came to 2.63 GB for the 2.15 GB of dZ_L, PMC)\n      float cs[SN / 2][NQ][2][4];  // [column pair][db_L, dw_head][subtile h][column r]\n#pragma unroll\n      for (int pp = 0; pp < SN / 2; ++pp)\n#pragma unroll\n        for (int q = 0; q < NQ; ++q)\n#pragma unroll\n          for (int h = 0; h < 2; ++h)\n#pragma unroll\n            for (int r = 0; r < 4; ++r) cs[pp][q][h][r] = 0.f;\n#pragma unroll\n      for (int j = 0; j < SM; ++j) {\n#pragma unroll\n        for (int pp = 0; pp < SN / 2; ++pp) {\n          uint2 dzp[2];\n#pragma unroll\n          for (int h = 0; h < 2; ++h) {\n            const int i = 2 * pp + h;\n            const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);\n            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};\n            float cf[4], yf[4];\n            const uint4 pk = __builtin_bit_cast(uint4, acc[i][j]);\n            const h16x4 yh = as_h4(uint2{pk.x, pk.y}), ch = as_h4(uint2{pk.z, pk.w});\n#pragma unroll\n            for (int r = 0; r < 4; ++r) {\n              yf[r] = (float)yh[r];\n              cf[r] = (float)ch[r];\n            }\n            float d[4];\n#pragma unroll\n            for (int r = 0; r < 4; ++r) {\n              const float dz = ((gm[j] * wv[r]) * cf[r]) * om;\n              cs[pp][0][h][r] += dz;\n              cs[pp][1][h][r] += gm[j] * yf[r];\n              d[r] = dz * S;\n            }\n            dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));\n          }\n          st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));\n        }\n      }\n#pragma unroll\n      for (int pp = 0; pp < SN / 2; ++pp)\n#pragma unroll\n        for (int q = 0; q < NQ; ++q)\n#pragma unroll\n          for (int h = 0; h < 2; ++h) {\n            float v[4];\n#pragma unroll\n            for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[pp][q][h][r]);\n            if ((lane & 15) == 0)\n              *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + (2 * pp + h) * 16 + 4 * (lane >> 4)) =\n                  float4{v[0], v[1], v[2], v[3]};\n          }\n"
+
 VARIANTS = {
     "noprio": {"gemm_pipeline.h": [(_PRIO_OLD1, _PRIO_NEW1), (_PRIO_OLD2, _PRIO_NEW2)]},
     "tnserp": {"gemm_tn.hip": [(_TNORD_OLD, _TNSERP_NEW)]},
@@ -280,6 +284,7 @@ VARIANTS = {
     "fl_nt": {"gemm_nt.hip": [(_ST16, _st16_asm("nt")), (_FL_OLD, _FL_NEW)]},  # whole-line non-temporal
     "st_l2": {"gemm_nt.hip": [(_L2ST_OLD, _L2ST_NEW)]},
     "hb_nowait": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW)]},
+    "hb_jouter": {"gemm_nt.hip": [(_HB_JO_OLD, _HB_JO_NEW)]},
     "hbs_ez": {"gemm_nt.hip": [(_HBS_EZ_OLD1, _HBS_EZ_NEW1), (_HBS_EZ_OLD2, _HBS_EZ_NEW2), (_HBS_EZ_OLD3, _HBS_EZ_NEW3)]},
     "hb_nopub": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW), (_HB_PUB_OLD, _HB_PUB_NEW)]},
     "hb_nopub_nostore": {"gemm_nt.hip": [(_HB_WAIT_OLD, _HB_WAIT_NEW), (_HB_PUB_OLD, _HB_PUB_NEW),
