@@ -485,26 +485,29 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         if (p.gmax_part) p.gmax_part[tm] = gx;
       }
       // ---- phase 2: head_bwd_kernel on the registers: dz = ((g w) C) omega stored x S (omega 1 for
-      // Snake / Tanh: C is their derivative), column partials of dz (db_L), of g Y (dw_head) and,
-      // Snake, of (g w) E (da_L) over the tile's rows.  Column pairs outermost (the 16-B dZ pieces
-      // pair adjacent subtiles), rows inside: each pair's accumulators and column partials die
-      // before the next pair's begin
+      // Snake / Tanh: C is their derivative), column partials of dz (db_L) and of g Y (dw_head) over
+      // the tile's rows
       constexpr int NQ = 2;  // db_L, dw_head here; a Snake's da_L in phase 3
       const float om = (MODE == NT_FWD_HB) ? p.omega : 1.0f, S = p.gscale[0];
       float gm[SM];
 #pragma unroll
       for (int j = 0; j < SM; ++j) gm[j] = g_lds[wm * TM + j * 16 + (lane & 15)];
+      // rows outermost, both column pairs of a row piece back to back: each 128-B row segment of
+      // dZ_L is then written whole by two consecutive stores (column pairs outermost wrote each
+      // line's halves a pass apart: the HBM writes came to 2.63 GB for the 2.15 GB of dZ_L, PMC)
+      float cs[SN / 2][NQ][2][4];  // [column pair][db_L, dw_head][subtile h][column r]
 #pragma unroll
-      for (int pp = 0; pp < SN / 2; ++pp) {
-        float cs[NQ][2][4];  // [db_L, dw_head][subtile h][column r]
+      for (int pp = 0; pp < SN / 2; ++pp)
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
 #pragma unroll
           for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) cs[q][h][r] = 0.f;
+            for (int r = 0; r < 4; ++r) cs[pp][q][h][r] = 0.f;
 #pragma unroll
-        for (int j = 0; j < SM; ++j) {
+      for (int j = 0; j < SM; ++j) {
+#pragma unroll
+        for (int pp = 0; pp < SN / 2; ++pp) {
           uint2 dzp[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
@@ -523,26 +526,28 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float dz = ((gm[j] * wv[r]) * cf[r]) * om;
-              cs[0][h][r] += dz;
-              cs[1][h][r] += gm[j] * yf[r];
+              cs[pp][0][h][r] += dz;
+              cs[pp][1][h][r] += gm[j] * yf[r];
               d[r] = dz * S;
             }
             dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
           }
           st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
         }
+      }
+#pragma unroll
+      for (int pp = 0; pp < SN / 2; ++pp)
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[q][h][r]);
+            for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[pp][q][h][r]);
             if ((lane & 15) == 0)
               *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + (2 * pp + h) * 16 + 4 * (lane >> 4)) =
                   float4{v[0], v[1], v[2], v[3]};
           }
-      }
       if constexpr (SNK) {
         // ---- phase 3 (Snake): da_L partials, sum over the tile's rows of (g w) E with E read back
         // from where phase 1 stored it (L2: written a hand-off earlier).  Every accumulator is dead
