@@ -300,6 +300,27 @@ VARIANTS = {
 }
 
 
+# Snake dX epilogue: Cprev / Eprev read non-temporally (streamed past L2), so that the two 2 GB
+# epilogue streams do not evict the K-loop's X / W tiles (NT_DX_SNAKE fetched 2.4x its operands)
+_DXS_NT_HELPER_OLD = "  auto st16 = [&](h16* dst, uint4 v) { *(uint4*)dst = v; };"
+_DXS_NT_HELPER_NEW = (_DXS_NT_HELPER_OLD + """
+  auto ldnt = [](const h16* src) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load((const u32x4*)src);
+    return uint4{v.x, v.y, v.z, v.w};
+  };""")
+_DXS_NT_OLD1 = """          ce_in[j][0] = *(const uint4*)(p.Cprev + off);
+          ce_in[j][1] = *(const uint4*)(p.Eprev + off);"""
+_DXS_NT_NEW1 = """          ce_in[j][0] = ldnt(p.Cprev + off);
+          ce_in[j][1] = ldnt(p.Eprev + off);"""
+_DXS_NT_OLD2 = """                cq[jj] = *(const uint4*)(p.Cprev + off);
+                eq[jj] = *(const uint4*)(p.Eprev + off);"""
+_DXS_NT_NEW2 = """                cq[jj] = ldnt(p.Cprev + off);
+                eq[jj] = ldnt(p.Eprev + off);"""
+VARIANTS["dxs_nt"] = {"gemm_nt.hip": [(_DXS_NT_HELPER_OLD, _DXS_NT_HELPER_NEW), (_DXS_NT_OLD1, _DXS_NT_NEW1),
+                                      (_DXS_NT_OLD2, _DXS_NT_NEW2)]}
+
+
 def build(name: str, extra_defines=()) -> str:
     patches = VARIANTS[name]
     out = os.path.join(ROOT, "inr-for-audio_amd", f"libsiren_{name}.so")
