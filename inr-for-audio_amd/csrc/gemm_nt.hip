@@ -42,7 +42,7 @@
 #define SIREN_SNAKE_EB 4
 #endif
 #ifndef SIREN_SNAKE0_EB
-#define SIREN_SNAKE0_EB 8
+#define SIREN_SNAKE0_EB 4
 #endif
 
 #ifdef SIREN_DIAG
@@ -274,14 +274,15 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // NT_DX / NT_DX0 epilogue operands loaded by `pre` (before the next tile's early prefetch).  The
   // rest are loaded by the epilogue in one batch once earlier pieces are consumed (their
   // accumulators free the registers), so a batch waits once, not once per piece behind the
-  // in-order vmcnt (which also covers the next tile's stages and this tile's stores).  NT_DX
-  // preloads every row; NT_DX0 rows 0 .. SM/2-1.  The Snake modes (Cprev AND Eprev per piece) go
-  // column pair by column pair: `pre` loads pair 0 of every row, the epilogue pair 1 after pair 0.
+  // in-order vmcnt (which also covers the next tile's stages and this tile's stores).  NT_DX and
+  // NT_DX0 preload every row (NT_DX0 has room for it since its products use v_fma_mix: 243 VGPRs,
+  // against 235 with half the rows before).  The Snake modes (Cprev AND Eprev per piece) go
+  // in batches of EB rows with both column pairs of a row together: `pre` loads pair 0 of the
+  // first batch.
   constexpr bool HAS_E = (MODE == NT_DX_SNAKE || MODE == NT_DX0_SNAKE);
-  constexpr int PRE_J = (nt_is_fwd(MODE) || HAS_E) ? 0 : (MODE == NT_DX ? SM : SM / 2);
-  // Snake modes: batches of EB rows of one column pair (pair 0 rows 0 .. EB-1 from `pre`)
-  // (fewest spills by the gfx950 listing: 4 for NT_DX_SNAKE -- 20-36 B against 144-160 B at 8 --,
-  // 8 for NT_DX0_SNAKE, whose partials of dW0 and da0 take the registers instead)
+  constexpr int PRE_J = (nt_is_fwd(MODE) || HAS_E) ? 0 : SM;
+  // Snake modes: EB = 4 rows per batch (gfx950 listing: 236 / 254 VGPRs for NT_DX_SNAKE /
+  // NT_DX0_SNAKE with no spills; 8 spills 128-176 B)
   constexpr int EB0 = (MODE == NT_DX0_SNAKE) ? SIREN_SNAKE0_EB : SIREN_SNAKE_EB;
   constexpr int EB = EB0 < SM ? EB0 : SM;
   static_assert(SM % EB == 0, "Snake epilogue batches");
@@ -514,22 +515,19 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             const int i = 2 * pp + h;
             const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);
             const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-            float cf[4], yf[4];
             const uint4 pk = __builtin_bit_cast(uint4, acc[i][j]);
-            const h16x4 yh = as_h4(uint2{pk.x, pk.y}), ch = as_h4(uint2{pk.z, pk.w});
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              yf[r] = (float)yh[r];
-              cf[r] = (float)ch[r];
-            }
+            const uint2 yh = uint2{pk.x, pk.y}, ch = uint2{pk.z, pk.w};
             float d[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float dz = ((gm[j] * wv[r]) * cf[r]) * om;
+            static_for<0, 4>([&](auto rc) {
+              constexpr int r = decltype(rc)::value;
+              // head_bwd_kernel's dz, ((g w) C) omega (bit-identical); omega is exactly 1 for a
+              // Snake / Tanh layer
+              float dz = mul_mix<r>(gm[j] * wv[r], ch);
+              if constexpr (MODE == NT_FWD_HB) dz *= om;
               cs[pp][0][h][r] += dz;
-              cs[pp][1][h][r] += gm[j] * yf[r];
+              cs[pp][1][h][r] = fma_mix<r>(gm[j], yh, cs[pp][1][h][r]);
               d[r] = dz * S;
-            }
+            });
             dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
           }
           st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
@@ -571,9 +569,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             for (int h = 0; h < 2; ++h) {
               const float4 w4 = *(const float4*)(hw_lds + nq + (2 * pp + h) * 16);
               const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-              const h16x4 eh = as_h4(eu[h]);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) da[h][r] += (gm[j] * wv[r]) * (float)eh[r];
+              static_for<0, 4>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                da[h][r] = fma_mix<r>(gm[j] * wv[r], eu[h], da[h][r]);
+              });
             }
           }
 #pragma unroll
@@ -746,49 +745,51 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int i = 2 * pp + h;
-          const h16x4 cp = as_h4(cpu[h]);
           float dz[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
+          static_for<0, 4>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            dz[r] = mul_mix<r>(acc[i][j][r], cpu[h]) * om;  // (acc C) omega
             cs[0][i][r] += dz[r];
             if constexpr (nt_is_dx0(MODE)) {
-              cs[1][i][r] += dz[r] * t0;
-              cs[2][i][r] += dz[r] * t1;
+              cs[1][i][r] = __builtin_fmaf(dz[r], t0, cs[1][i][r]);
+              cs[2][i][r] = __builtin_fmaf(dz[r], t1, cs[2][i][r]);
             }
-            if constexpr (MODE == NT_DX_SNAKE) cs[1][i][r] += acc[i][j][r] * (float)as_h4(epu[h])[r];
-            if constexpr (MODE == NT_DX0_SNAKE) cs[3][i][r] += acc[i][j][r] * (float)as_h4(epu[h])[r];
-          }
+            if constexpr (MODE == NT_DX_SNAKE) cs[1][i][r] = fma_mix<r>(acc[i][j][r], epu[h], cs[1][i][r]);
+            if constexpr (MODE == NT_DX0_SNAKE) cs[3][i][r] = fma_mix<r>(acc[i][j][r], epu[h], cs[3][i][r]);
+          });
           dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
         }
         if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE)
           st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
       };
       if constexpr (HAS_E) {
+        // batches of EB rows, both column pairs of a row back to back: the two 64-B halves of each
+        // row's 128-B Cprev / Eprev / dZ segments are read and written together (pair 0 of the
+        // first EB rows comes from `pre`)
         static_assert(SN == 4, "two column pairs");
-        static_for<0, 2>([&](auto ppc) {
-          constexpr int pp = decltype(ppc)::value;
-          static_for<0, SM / EB>([&](auto bqc) {
-            constexpr int bq = decltype(bqc)::value;
-            if constexpr (pp == 0 && bq == 0) {
-              static_for<0, EB>([&](auto jc) { piece(jc, ppc, ce_in[decltype(jc)::value][0], ce_in[decltype(jc)::value][1]); });
-            } else {
-              uint4 cq[EB], eq[EB];
+        static_for<0, SM / EB>([&](auto bqc) {
+          constexpr int bq = decltype(bqc)::value;
+          uint4 cq[EB][2], eq[EB][2];
 #pragma unroll
-              for (int jj = 0; jj < EB; ++jj) {
+          for (int jj = 0; jj < EB; ++jj)
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+              if (bq == 0 && pp == 0) {
+                cq[jj][pp] = ce_in[jj][0];
+                eq[jj][pp] = ce_in[jj][1];
+              } else {
                 const size_t off = (size_t)(mrow0 + (bq * EB + jj) * 16) * N + npc + pp * 32;
-                cq[jj] = *(const uint4*)(p.Cprev + off);
-                eq[jj] = *(const uint4*)(p.Eprev + off);
+                cq[jj][pp] = *(const uint4*)(p.Cprev + off);
+                eq[jj][pp] = *(const uint4*)(p.Eprev + off);
               }
-              static_for<0, EB>([&](auto jc) {
-                constexpr int jj = decltype(jc)::value;
-                piece(std::integral_constant<int, bq * EB + jj>{}, ppc, cq[jj], eq[jj]);
-              });
             }
+          static_for<0, EB>([&](auto jc) {
+            constexpr int jj = decltype(jc)::value;
+            piece(std::integral_constant<int, bq * EB + jj>{}, std::integral_constant<int, 0>{}, cq[jj][0], eq[jj][0]);
+            piece(std::integral_constant<int, bq * EB + jj>{}, std::integral_constant<int, 1>{}, cq[jj][1], eq[jj][1]);
           });
-          flush(std::integral_constant<int, 2 * pp>{});  // this pair's column partials are final
-          flush(std::integral_constant<int, 2 * pp + 1>{});
         });
+        static_for<0, SN>([&](auto ic) { flush(ic); });
       } else {
         // NT_DX / NT_DX0: rows in order, both column pairs of a row together (rows >= PRE_J loaded
         // at use), then the column partials.  The same arithmetic as `piece`, kept as a plain loop:
@@ -811,17 +812,16 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const int i = 2 * pp + h;
-              const h16x4 cp = as_h4(cpu[h]);
               float dz[4];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                dz[r] = (acc[i][j][r] * (float)cp[r]) * om;
+              static_for<0, 4>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                dz[r] = mul_mix<r>(acc[i][j][r], cpu[h]) * om;  // (acc C) omega
                 cs[0][i][r] += dz[r];
                 if constexpr (nt_is_dx0(MODE)) {
-                  cs[1][i][r] += dz[r] * t0;
-                  cs[2][i][r] += dz[r] * t1;
+                  cs[1][i][r] = __builtin_fmaf(dz[r], t0, cs[1][i][r]);
+                  cs[2][i][r] = __builtin_fmaf(dz[r], t1, cs[2][i][r]);
                 }
-              }
+              });
               dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
             }
             if constexpr (MODE == NT_DX) st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));

@@ -131,6 +131,25 @@ __device__ __forceinline__ int swap16_col(int lane) { return ((lane >> 4) & 1) *
 __device__ __forceinline__ uint2 as_u2(h16x4 v) { return __builtin_bit_cast(uint2, v); }
 __device__ __forceinline__ h16x4 as_h4(uint2 v) { return __builtin_bit_cast(h16x4, v); }
 
+// a * (float)h + c, h = fp16 element R of a packed 4-element piece, in one v_fma_mix_f32: the
+// instruction widens the fp16 operand exactly, so the result is the one of a v_cvt_f32_f16 and a
+// v_fma_f32, with one VALU instead of two.  `volatile` keeps the statements in program order:
+// left free, the scheduler hoists them in a cluster ahead of their consumers and spills.
+template <int R>
+__device__ __forceinline__ float fma_mix(float a, uint2 piece, float c) {
+  static_assert(R >= 0 && R < 4, "element of a 4-element piece");
+  const unsigned w = R < 2 ? piece.x : piece.y;
+  float r;
+  if constexpr (R & 1)
+    asm volatile("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(w), "v"(c));
+  else
+    asm volatile("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(w), "v"(c));
+  return r;
+}
+// a * (float)h exactly (fma with a -0 addend: x + -0 = x for every x, signed zeros included)
+template <int R>
+__device__ __forceinline__ float mul_mix(float a, uint2 piece) { return fma_mix<R>(a, piece, -0.0f); }
+
 // Sum over the 16 lanes of a DPP row (lanes with equal lane>>4): fixed rotation order, result
 // in every lane of the row.
 __device__ __forceinline__ float row16_sum(float v) {
