@@ -110,13 +110,7 @@ __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const 
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       if constexpr (SNAKE) {
-        const float z = first_preact(in_dim, t0, t1, w0[r], w1[r], bb[r]);
-        float sn, cn;
-        sincos_rev(z * av[r], &sn, &cn);
-        const float ia = 1.0f / av[r], s2 = sn * sn, sc2 = 2.0f * sn * cn;
-        y[r] = z + s2 * ia;
-        c[r] = 1.0f + sc2;
-        ev[r] = (z * sc2 - s2 * ia) * ia;
+        snake_epi(first_preact(in_dim, t0, t1, w0[r], w1[r], bb[r]), av[r], 1.0f / av[r], y[r], c[r], ev[r]);
         continue;
       }
       sincos_rev(omega0 * first_preact(in_dim, t0, t1, w0[r], w1[r], bb[r]), &y[r], &c[r]);

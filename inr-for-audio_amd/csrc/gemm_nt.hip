@@ -365,14 +365,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               float cv[4], ev[4];
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const float z = acc[i][j][r] + bb[r];
-                const float ia = iav[r];
-                const float x = __builtin_amdgcn_fractf((z * av[r]) * kInv2Pi);  // a z in revolutions
-                const float sn = __builtin_amdgcn_sinf(x), cn = __builtin_amdgcn_cosf(x);
-                const float s2 = sn * sn, sc2 = 2.0f * sn * cn;
-                sv[r] = z + s2 * ia;               // models.py:241
-                cv[r] = 1.0f + sc2;                // dY/dz
-                ev[r] = (z * sc2 - s2 * ia) * ia;  // dY/da
+                snake_epi(acc[i][j][r] + bb[r], av[r], iav[r], sv[r], cv[r], ev[r]);
               }
               // Y and D packed in place of the accumulators; E goes to HBM (p.E, the layer's E
               // buffer) in 16-B row pieces once both subtiles of the pair have it, and phase 3 reads
@@ -641,14 +634,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               const float av[4] = {a4.x, a4.y, a4.z, a4.w}, iav[4] = {ia4.x, ia4.y, ia4.z, ia4.w};
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const float z = acc[i][j][r] + bb[r];
-                const float ia = iav[r];
-                const float x = __builtin_amdgcn_fractf((z * av[r]) * kInv2Pi);  // a z in revolutions
-                const float sn = __builtin_amdgcn_sinf(x), cn = __builtin_amdgcn_cosf(x);
-                const float s2 = sn * sn, sc2 = 2.0f * sn * cn;
-                s[r] = z + s2 * ia;                    // models.py:241
-                c[r] = 1.0f + sc2;                     // dY/dz
-                e[r] = (z * sc2 - s2 * ia) * ia;       // dY/da
+                snake_epi(acc[i][j][r] + bb[r], av[r], iav[r], s[r], c[r], e[r]);
               }
             } else {  // NT_FWD_TANH
 #pragma unroll

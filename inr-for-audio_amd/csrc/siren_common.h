@@ -17,6 +17,20 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 namespace siren {
 
 constexpr float kInv2Pi = 0.15915494309189535f;  // 1/(2*pi), rounded to fp32
+constexpr float kInvPi = 0.31830988618379067f;   // 1/pi, rounded to fp32
+
+// Snake y = z + sin^2(a z)/a (models.py:241) with dY/dz = 1 + sin(2az) and dY/da =
+// (z sin(2az) - sin^2(az)/a)/a, from the double angle: sin^2(az) = (1 - cos 2az)/2, so one
+// sin / cos pair of 2az (in revolutions) and 7 other VALU, where the single-angle form takes 11.
+// Same absolute error (the fp16 outputs and the fp32 argument bound it); ia = 1/a.
+__device__ __forceinline__ void snake_epi(float z, float a, float ia, float& y, float& d, float& e) {
+  const float x = __builtin_amdgcn_fractf((z * a) * kInvPi);  // 2 a z in revolutions
+  const float s = __builtin_amdgcn_sinf(x), c = __builtin_amdgcn_cosf(x);
+  const float t = __builtin_fmaf(-0.5f, c, 0.5f) * ia;  // sin^2(a z) / a
+  y = z + t;
+  d = 1.0f + s;
+  e = __builtin_fmaf(z, s, -t) * ia;
+}
 
 // Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle
 // must be bijective"): blocks b, b+8, b+16 ... are dealt to one XCD, so consecutive
