@@ -519,7 +519,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               if constexpr (MODE == NT_FWD_HB) dz *= om;
               cs[pp][0][h][r] += dz;
               cs[pp][1][h][r] = fma_mix<r>(gm[j], yh, cs[pp][1][h][r]);
-              d[r] = dz * S;
+              d[r] = dz * S;  // S is a power of two: exact, however hipcc rounds it to fp16
             });
             dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
           }
@@ -534,7 +534,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int h = 0; h < 2; ++h) {
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[pp][q][h][r]);
+            for (int r = 0; r < 4; ++r) v[r] = cs[pp][q][h][r];
+            row16_sum4(v);
             if ((lane & 15) == 0)
               *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + (2 * pp + h) * 16 + 4 * (lane >> 4)) =
                   float4{v[0], v[1], v[2], v[3]};
@@ -572,7 +573,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int h = 0; h < 2; ++h) {
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = row16_sum(da[h][r]);
+            for (int r = 0; r < 4; ++r) v[r] = da[h][r];
+            row16_sum4(v);
             if ((lane & 15) == 0)
               *(float4*)(red + (2 * Cfg::WM + wm) * BN + wn * TN + (2 * pp + h) * 16 + 4 * (lane >> 4)) =
                   float4{v[0], v[1], v[2], v[3]};
@@ -707,7 +709,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           const bool da0 = (MODE == NT_DX0_SNAKE) && q == nred - 1;
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = row16_sum(da0 ? cs[3][i][r] : cs[q][i][r]);
+          for (int r = 0; r < 4; ++r) v[r] = da0 ? cs[3][i][r] : cs[q][i][r];
+          row16_sum4(v);
           if ((lane & 15) == 0)
             *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + i * 16 + 4 * (lane >> 4)) =
                 float4{v[0], v[1], v[2], v[3]};
@@ -735,6 +738,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           static_for<0, 4>([&](auto rc) {
             constexpr int r = decltype(rc)::value;
             dz[r] = mul_mix<r>(acc[i][j][r], cpu[h]) * om;  // (acc C) omega
+            asm volatile("" : "+v"(dz[r]));  // rounded to fp32 before the fp16 store (fp32_first)
             cs[0][i][r] += dz[r];
             if constexpr (nt_is_dx0(MODE)) {
               cs[1][i][r] = __builtin_fmaf(dz[r], t0, cs[1][i][r]);
@@ -802,6 +806,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               static_for<0, 4>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
                 dz[r] = mul_mix<r>(acc[i][j][r], cpu[h]) * om;  // (acc C) omega
+                asm volatile("" : "+v"(dz[r]));  // rounded to fp32 before the fp16 store (fp32_first)
                 cs[0][i][r] += dz[r];
                 if constexpr (nt_is_dx0(MODE)) {
                   cs[1][i][r] = __builtin_fmaf(dz[r], t0, cs[1][i][r]);
@@ -820,7 +825,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int i = 0; i < SN; ++i) {
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = row16_sum(cs[q][i][r]);
+            for (int r = 0; r < 4; ++r) v[r] = cs[q][i][r];
+            row16_sum4(v);
             if ((lane & 15) == 0)
               *(float4*)(red + (q * Cfg::WM + wm) * BN + wn * TN + i * 16 + 4 * (lane >> 4)) =
                   float4{v[0], v[1], v[2], v[3]};

@@ -145,6 +145,11 @@ __device__ __forceinline__ int swap16_col(int lane) { return ((lane >> 4) & 1) *
 __device__ __forceinline__ uint2 as_u2(h16x4 v) { return __builtin_bit_cast(uint2, v); }
 __device__ __forceinline__ h16x4 as_h4(uint2 v) { return __builtin_bit_cast(h16x4, v); }
 
+// fp32_first: an empty asm on a value that is stored as fp16 keeps its fp32 rounding.  Left alone,
+// hipcc folds some (x * y) -> fp16 pairs into one v_fma_mixlo_f16, a single rounding, and which
+// pairs it folds changes from build to build; the oracle and the fp32 column partials see the
+// fp32 value.  Applied to the dX epilogues' (acc C) omega; a product by the power-of-two dZ scale
+// is exact, so its fold changes nothing.
 // a * (float)h + c, h = fp16 element R of a packed 4-element piece, in one v_fma_mix_f32: the
 // instruction widens the fp16 operand exactly, so the result is the one of a v_cvt_f32_f16 and a
 // v_fma_f32, with one VALU instead of two.  `volatile` keeps the statements in program order:
@@ -172,6 +177,35 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));
   return v;
+}
+
+// row16_sum of four values at once, one v_add_f32 with a DPP row_ror source per value and step
+// (the same sums, bit for bit).  Written with the builtin, hipcc pairs the four chains' adds into
+// v_pk_add_f32 and moves every DPP result into a register pair first: three instructions per add.
+// The four chains are interleaved, so a chain's DPP read is three VALU after its last write (the
+// gfx950 VALU-write -> DPP-read hazard needs two wait states); the leading s_nop covers the
+// compiler's last write of an input.
+__device__ __forceinline__ void row16_sum4(float (&v)[4]) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %2, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %3, %3, %3 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %2, %2, %2 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %3, %3, %3 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %0, %0, %0 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %2, %2, %2 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %3, %3, %3 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %0, %0, %0 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %2, %2, %2 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %3, %3, %3 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1"
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
 }
 
 // Block-wide sum of one float per thread (blockDim.x multiple of 64, <= 1024).
