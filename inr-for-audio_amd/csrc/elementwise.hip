@@ -80,8 +80,8 @@ hipError_t coords_fill_grid(float* xy, int64_t rows, int64_t offset, int64_t hei
 // adds < 2e-4 rev with 2^-24 relative error, so r is within ~4e-8 rev (2.5e-7 rad) of a/(2pi)
 // mod 1 for every |a| < 2^17.  v_sin_f32 / v_cos_f32 take revolutions directly.  (OCML's
 // sincosf with its large-argument reduction made this kernel VALU-bound at 2.1 ms.)
-// (sincos_rev / first_preact live in siren_common.h: the dX GEMM's NT_DX0R epilogue
-// recomputes the same cosine.)
+// (sincos_rev / first_preact live in siren_common.h.  A layer-0 dX epilogue that recomputed this
+// cosine instead of reading C0 was measured in round 2 and removed: DESIGN §4.)
 // Row-wise: each thread owns 8 columns (W0 / b0 in registers) and walks rows; a row is H/8
 // threads, a 256-thread block covers 256/(H/8) rows per pass; Y0 / C0 go out as 16-B pieces.
 // SNAKE (first_linear=True, models.py:330-333): Linear(in, H) + Snake(a0) --
