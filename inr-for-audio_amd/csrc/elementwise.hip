@@ -103,9 +103,21 @@ __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const 
     bb[r] = b0[n + r];
     av[r] = SNAKE ? a0[n + r] : 0.f;
   }
-  for (int64_t m = (int64_t)blockIdx.x * rpb + lr; m < R; m += (int64_t)gridDim.x * rpb) {
-    const float t0 = t[m * in_dim];
-    const float t1 = (in_dim > 1) ? t[m * in_dim + 1] : 0.f;
+  // the next row's coordinates are loaded before this row's stores: vmcnt retires loads and
+  // stores in issue order, so a load issued after the stores would wait for them too
+  const int64_t stride = (int64_t)gridDim.x * rpb;
+  int64_t m = (int64_t)blockIdx.x * rpb + lr;
+  float t0n = 0.f, t1n = 0.f;
+  if (m < R) {
+    t0n = t[m * in_dim];
+    if (in_dim > 1) t1n = t[m * in_dim + 1];
+  }
+  for (; m < R; m += stride) {
+    const float t0 = t0n, t1 = t1n;
+    if (m + stride < R) {
+      t0n = t[(m + stride) * in_dim];
+      if (in_dim > 1) t1n = t[(m + stride) * in_dim + 1];
+    }
     float y[8], c[8], ev[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
