@@ -39,10 +39,10 @@
 
 // rows per Cprev/Eprev batch in the Snake dX epilogues (gemm_nt_kernel): NT_DX_SNAKE, NT_DX0_SNAKE
 #ifndef SIREN_SNAKE_EB
-#define SIREN_SNAKE_EB 4
+#define SIREN_SNAKE_EB 2
 #endif
 #ifndef SIREN_SNAKE0_EB
-#define SIREN_SNAKE0_EB 4
+#define SIREN_SNAKE0_EB 2
 #endif
 
 #ifdef SIREN_DIAG
@@ -281,8 +281,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // first batch.
   constexpr bool HAS_E = (MODE == NT_DX_SNAKE || MODE == NT_DX0_SNAKE);
   constexpr int PRE_J = (nt_is_fwd(MODE) || HAS_E) ? 0 : SM;
-  // Snake modes: EB = 4 rows per batch (gfx950 listing: 236 / 254 VGPRs for NT_DX_SNAKE /
-  // NT_DX0_SNAKE with no spills; 8 spills 128-176 B)
+  // Snake modes: EB = 2 rows per batch, two batches in flight (gfx950 listing: 238 / 247 VGPRs
+  // for NT_DX_SNAKE / NT_DX0_SNAKE, no spills; 4 rows spill 164-196 B): dX Snake 2.559 -> 2.530 ms
+  // against 4-row batches loaded at use (profiles/r16c/ab_snake_dx_pipelined.json)
   constexpr int EB0 = (MODE == NT_DX0_SNAKE) ? SIREN_SNAKE0_EB : SIREN_SNAKE_EB;
   constexpr int EB = EB0 < SM ? EB0 : SM;
   static_assert(SM % EB == 0, "Snake epilogue batches");
@@ -757,26 +758,33 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         // row's 128-B Cprev / Eprev / dZ segments are read and written together (pair 0 of the
         // first EB rows comes from `pre`)
         static_assert(SN == 4, "two column pairs");
-        static_for<0, SM / EB>([&](auto bqc) {
-          constexpr int bq = decltype(bqc)::value;
-          uint4 cq[EB][2], eq[EB][2];
+        // software-pipelined: batch bq+1 is loaded before batch bq's dZ stores go out, so waiting
+        // for a batch never waits for earlier stores (vmcnt retires in issue order)
+        uint4 cq[2][EB][2], eq[2][EB][2];  // [buffer][row][column pair]
+        auto load_batch = [&](auto bqc) {
+          constexpr int bq = decltype(bqc)::value, bf = bq & 1;
 #pragma unroll
           for (int jj = 0; jj < EB; ++jj)
 #pragma unroll
             for (int pp = 0; pp < 2; ++pp) {
               if (bq == 0 && pp == 0) {
-                cq[jj][pp] = ce_in[jj][0];
-                eq[jj][pp] = ce_in[jj][1];
+                cq[bf][jj][pp] = ce_in[jj][0];
+                eq[bf][jj][pp] = ce_in[jj][1];
               } else {
                 const size_t off = (size_t)(mrow0 + (bq * EB + jj) * 16) * N + npc + pp * 32;
-                cq[jj][pp] = *(const uint4*)(p.Cprev + off);
-                eq[jj][pp] = *(const uint4*)(p.Eprev + off);
+                cq[bf][jj][pp] = *(const uint4*)(p.Cprev + off);
+                eq[bf][jj][pp] = *(const uint4*)(p.Eprev + off);
               }
             }
+        };
+        load_batch(std::integral_constant<int, 0>{});
+        static_for<0, SM / EB>([&](auto bqc) {
+          constexpr int bq = decltype(bqc)::value, bf = bq & 1;
+          if constexpr (bq + 1 < SM / EB) load_batch(std::integral_constant<int, bq + 1>{});
           static_for<0, EB>([&](auto jc) {
             constexpr int jj = decltype(jc)::value;
-            piece(std::integral_constant<int, bq * EB + jj>{}, std::integral_constant<int, 0>{}, cq[jj][0], eq[jj][0]);
-            piece(std::integral_constant<int, bq * EB + jj>{}, std::integral_constant<int, 1>{}, cq[jj][1], eq[jj][1]);
+            piece(std::integral_constant<int, bq * EB + jj>{}, std::integral_constant<int, 0>{}, cq[bf][jj][0], eq[bf][jj][0]);
+            piece(std::integral_constant<int, bq * EB + jj>{}, std::integral_constant<int, 1>{}, cq[bf][jj][1], eq[bf][jj][1]);
           });
         });
         static_for<0, SN>([&](auto ic) { flush(ic); });
