@@ -499,8 +499,16 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int r = 0; r < 4; ++r) cs[pp][q][h][r] = 0.f;
+      // Snake: row j's E pieces are loaded as phase 2 reaches row j, ahead of its dZ_L stores (the
+      // registers of row j's accumulators free up as it goes); phase 3 reads them from registers
+      uint4 eall[SNK ? SM : 1][SNK ? SN / 2 : 1];
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
+        if constexpr (SNK) {
+#pragma unroll
+          for (int pp = 0; pp < SN / 2; ++pp)
+            eall[j][pp] = *(const uint4*)(p.E + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
+        }
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
           uint2 dzp[2];
@@ -542,15 +550,13 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                   float4{v[0], v[1], v[2], v[3]};
           }
       if constexpr (SNK) {
-        // ---- phase 3 (Snake): da_L partials, sum over the tile's rows of (g w) E with E read back
-        // from where phase 1 stored it (L2: written a hand-off earlier).  Every accumulator is dead
-        // by now, so a column pair's 8 row pieces are loaded in one batch (one wait, which also
-        // drains the dZ stores ahead of it in the in-order vmcnt)
+        // ---- phase 3 (Snake): da_L partials, sum over the tile's rows of (g w) E, with E read back
+        // from where phase 1 stored it (L2: written a hand-off earlier) during phase 2
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
           uint4 eq[SM];
 #pragma unroll
-          for (int j = 0; j < SM; ++j) eq[j] = *(const uint4*)(p.E + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
+          for (int j = 0; j < SM; ++j) eq[j] = eall[j][pp];
           float da[2][4];
 #pragma unroll
           for (int h = 0; h < 2; ++h)
