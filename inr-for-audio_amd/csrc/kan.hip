@@ -509,10 +509,23 @@ __global__ __launch_bounds__(256) void kan_head_train_kernel(const float* __rest
     for (int c = 0; c < KAN_NB; ++c) ws[c] = W[in + KAN_NB * lane + c];
   }
   float ab = 0.f, as[KAN_NB] = {}, sse = 0.f;
-  for (int64_t n = nb + wv; n < ne; n += 4) {
+  // the next row's x and y are loaded before this row's stores: vmcnt retires loads and stores in
+  // issue order, so a load issued after the stores would wait for them too
+  int64_t n = nb + wv;
+  float xn = 0.f, yn = 0.f;
+  if (n < ne) {
+    if (on) xn = X[n * in + lane];
+    if (n < n_valid) yn = y[n];
+  }
+  for (; n < ne; n += 4) {
+    const float xc = xn, yc = yn;
+    if (n + 4 < ne) {
+      if (on) xn = X[(n + 4) * in + lane];
+      if (n + 4 < n_valid) yn = y[n + 4];
+    }
     float x = 0.f, v = 0.f, sl = 0.f, b[KAN_NB], db[KAN_NB];
     if (on) {
-      x = X[n * in + lane];
+      x = xc;
       kan_bases_local<true, false, false>(x, gk[lane], b, db, inv[lane]);  // lane-fixed knots: selects
       sl = silu(x);
       v = sl * wb;
@@ -523,7 +536,7 @@ __global__ __launch_bounds__(256) void kan_head_train_kernel(const float* __rest
     const float o = (0.f + v) + 0.f;  // head_loss's accumulation of the one partial and the zero bias
     float gn = 0.f;
     if (n < n_valid) {
-      const float err = o - y[n];
+      const float err = o - yc;
       sse += err * err;
       gn = err * gfac;
     }
