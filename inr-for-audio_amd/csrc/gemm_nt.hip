@@ -275,10 +275,11 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // rest are loaded by the epilogue in one batch once earlier pieces are consumed (their
   // accumulators free the registers), so a batch waits once, not once per piece behind the
   // in-order vmcnt (which also covers the next tile's stages and this tile's stores).  NT_DX and
-  // NT_DX0 preload every row (NT_DX0 has room for it since its products use v_fma_mix: 243 VGPRs,
-  // against 235 with half the rows before).  The Snake modes (Cprev AND Eprev per piece) go
-  // in batches of EB rows with both column pairs of a row together: `pre` loads pair 0 of the
-  // first batch.
+  // NT_DX0 preload every row (NT_DX0 has room for it since its products use v_fma_mix and its
+  // row sums v_add_f32_dpp: 229 VGPRs, against 235 with half the rows before).  The Snake modes
+  // (Cprev AND Eprev per piece) go in batches of EB rows with both column pairs of a row
+  // together: `pre` loads pair 0 of the first batch, and each batch loads the next one before
+  // its own dZ stores.
   constexpr bool HAS_E = (MODE == NT_DX_SNAKE || MODE == NT_DX0_SNAKE);
   constexpr int PRE_J = (nt_is_fwd(MODE) || HAS_E) ? 0 : SM;
   // Snake modes: EB = 2 rows per batch, two batches in flight (gfx950 listing: 238 / 247 VGPRs
