@@ -126,7 +126,9 @@ constexpr bool nt_is_dx0(int m) { return m == NT_DX0 || m == NT_DX0_SNAKE; }
 
 // tanh for the fp16-stored Tanh epilogues (NT_FWD_TANH, NT_FWD_HB_TANH), branch-free on the hardware
 // exp2 / rcp: sign(x) (1 - e) / (1 + e) with e = exp(-2|x|) (a few fp32 ulp), and the odd Taylor
-// polynomial below |x| < 1/16 where 1 - e would cancel (relative error < 1e-9 there).  ocml's tanhf
+// polynomial below |x| < 1/16 where 1 - e would cancel.  Its x^7 term is below fp32 resolution
+// there (2e-9 relative), so it stops at x^5: max relative error 8.7e-8, the fp32 rounding floor,
+// with fp16 outputs equal to the degree-7 form's on 200 k points of [0, 1/16].  ocml's tanhf
 // is branchy and its temporaries made the fused Tanh head spill 184 B per lane; the outputs are
 // stored in fp16 (2^-11), where the two agree to within the parity tests' fp16 bounds.
 __device__ __forceinline__ float tanh_epi(float x) {
@@ -134,7 +136,7 @@ __device__ __forceinline__ float tanh_epi(float x) {
   const float e = __builtin_amdgcn_exp2f(ax * -2.8853900817779268f);  // exp(-2|x|) = 2^(-2|x| / ln 2)
   const float big = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
   const float x2 = ax * ax;
-  const float small = ax * (1.0f + x2 * (-0.33333333f + x2 * (0.13333334f + x2 * -0.053968254f)));
+  const float small = ax * (1.0f + x2 * (-0.33333333f + x2 * 0.13333334f));
   return __builtin_copysignf(ax < 0.0625f ? small : big, x);
 }
 
