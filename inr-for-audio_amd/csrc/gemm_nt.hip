@@ -336,9 +336,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       // tile, summed exactly as NT_FWD(_SNAKE/_TANH) + HEAD sums them.  Sine / Tanh: Y and C (= cos,
       // or 1 - Y^2) rounded to fp16 as the unfused forward stores them, packed IN PLACE of their
       // accumulators (4 fp32 -> 4 + 4 fp16: the same 4 VGPRs, so nothing more is live across the
-      // hand-off than the accumulators).  Snake has three fp16 outputs (Y, D, E), which do not fit
-      // there: the accumulators stay as they are and phase 2 re-evaluates the same expressions
-      // (bit-identical: the same operations on the same operands).
+      // hand-off than the accumulators).  Snake has three fp16 outputs (Y, D, E): Y and D go in
+      // place of the accumulators, E to the layer's E buffer, read back during phase 2.
       constexpr bool SNK = MODE == NT_FWD_HB_SNAKE, TNH = MODE == NT_FWD_HB_TANH;
       const int nq = n0 + wn * TN + 4 * (lane >> 4);
       const float xs = (MODE == NT_FWD_HB) ? p.omega * kInv2Pi : 1.0f;
