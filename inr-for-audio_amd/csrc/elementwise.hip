@@ -176,7 +176,7 @@ __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts
                                  float* __restrict__ g, float* __restrict__ sse_part,
                                  float* __restrict__ gsum_part, float* __restrict__ gmax_part,
                                  float head_omega, int loss_mode) {
-  __shared__ float scratch[4];
+  __shared__ float scratch[12];  // 3 x (256 / 64) (block_sum2_max)
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   float e2 = 0.f, gv = 0.f;
   if (m < R) {
@@ -201,9 +201,8 @@ __global__ void head_loss_kernel(const float* __restrict__ head_part, int nparts
     }
     g[m] = gv;
   }
-  const float se = block_sum(e2, scratch);
-  const float gs = block_sum(gv, scratch);
-  const float gm = block_max(fabsf(gv), scratch);
+  float se = e2, gs = gv, gm = fabsf(gv);
+  block_sum2_max(se, gs, gm, scratch);
   if (threadIdx.x == 0) {
     sse_part[blockIdx.x] = se;
     gsum_part[blockIdx.x] = gs;

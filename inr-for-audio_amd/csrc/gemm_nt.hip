@@ -472,10 +472,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       // the band's loss and bias-gradient partials (head_loss_kernel's 256-row blocks and sums;
       // threads >= BM add zeros); the block sums' barriers also publish g_lds.  max|g| of the band
       // (head_loss_kernel's gmax partial): the next launch's backward scale for a Snake last layer
-      const float se = block_sum(e2, g_lds + BM);
-      const float gs = block_sum(gv, g_lds + BM);
-      float gx = 0.f;
-      if (p.gmax_part) gx = block_max(fabsf(gv), g_lds + BM);
+      float se = e2, gs = gv, gx = fabsf(gv);
+      block_sum2_max(se, gs, gx, g_lds + BM);
       if (tn == 0 && tid == 0) {
         p.sse_part[tm] = se;
         p.gsum_part[tm] = gs;

@@ -221,6 +221,34 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return s;
 }
 
+// block_sum(a), block_sum(b) and block_max(c) in one pass: every value keeps its own reduction
+// tree (the same results, bit for bit, as the three calls), with the three shuffle chains
+// interleaved and one pair of barriers instead of three.  scratch: 3 * blockDim.x / 64 floats.
+__device__ __forceinline__ void block_sum2_max(float& a, float& b, float& c, float* scratch) {
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+    c = fmaxf(c, __shfl_xor(c, o, 64));
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    scratch[w] = a;
+    scratch[nw + w] = b;
+    scratch[2 * nw + w] = c;
+  }
+  __syncthreads();
+  float s = 0.f, t = 0.f, m = 0.f;
+  for (int i = 0; i < nw; ++i) {  // fixed order: deterministic
+    s += scratch[i];
+    t += scratch[nw + i];
+    m = fmaxf(m, scratch[2 * nw + i]);
+  }
+  a = s;
+  b = t;
+  c = m;
+}
+
 // Block-wide max, same contract as block_sum.
 __device__ __forceinline__ float block_max(float v, float* scratch) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
