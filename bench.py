@@ -192,6 +192,92 @@ def profiled_steps(eng, args, dev, dist, lib, _lib, records_per_step, dom_of):
     return elapsed, breakdown, prof_steps, dom, timed
 
 
+def dp_report(eng, args, dev, dist, steps: int = 5) -> dict:
+    """What a data-parallel run saw, measured after the timed region: the process group's backend
+    and world size as torch.distributed reports them, the step with and without the gradient
+    all-reduce (comm_enabled off: the same launches minus the exchange; timing only, the ranks'
+    weights drift apart afterwards), the difference = the all-reduce time NOT hidden under the
+    backward (max over ranks), and the all-reduce of the whole flat gradient vector alone."""
+    def timed(fn, k):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        e = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        return float(e.item()) / k * 1e3
+
+    with_comm = timed(eng.step, steps)
+    eng.comm_enabled = False
+    try:
+        without = timed(eng.step, steps)
+    finally:
+        eng.comm_enabled = True
+    alone = timed(lambda: dist.all_reduce(eng.grads), steps)
+    return {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(),
+            "rccl": dist.get_backend() == "nccl", "bucketed_overlap": eng._buckets is not None,
+            "buckets": len(eng._buckets or []), "allreduce_bytes": eng.grads.numel() * 4,
+            "ms_per_step_with_allreduce": with_comm, "ms_per_step_without_allreduce": without,
+            "exposed_allreduce_ms_per_step": with_comm - without, "allreduce_alone_ms": alone,
+            "steps": steps,
+            "note": "after the timed region; exposed = step with the bucketed all-reduce minus the same step "
+                    "without it (max over ranks)"}
+
+
+# recon SNR fixtures (the metric's second half), newest first: the reference's own fit of the
+# headline model on gt_bach, written by tests/golden/make_golden.py in the build container
+RECON_FIXTURES = [("fit_5x1024_6s_converged.json", "gt_bach_6s.npz"),
+                  ("trajectory_5x1024_w3000_lr3e-5_seeds.json", "gt_bach_1s.npz")]
+
+
+def recon_snr(dev) -> dict | None:
+    """BASELINE's "recon SNR dB" on the bench line (outside the timed region): the headline model
+    (SIREN 5x1024) fitted on the fixture's clip with the fixture's hyper-parameters, seed 0, then
+    SNR_target of the final weights (utils.py:77-97 calculate_snr(target, model(coords)), the
+    quantity run.py:302-335 reports) next to the reference's own value for the same run."""
+    import numpy as np
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    from inr_for_audio_amd.utils import calculate_snr, get_coord
+    gdir = os.path.join(ROOT, "tests", "golden")
+    for fname, tname in RECON_FIXTURES:
+        path = os.path.join(gdir, fname)
+        if os.path.exists(path):
+            break
+    else:
+        return None
+    ref = json.load(open(path))
+    run = ref["runs"]["0"]
+    target = np.load(os.path.join(gdir, tname))["target"].astype(np.float32)
+    coords = get_coord(target.size, 1).reshape(-1, 1)
+    torch.manual_seed(0)
+    model = SirenWithSnakeTanh(1, 1, ref["hidden"], ref["num_sine"], 0, 0, first_omega_0=ref["omega0"],
+                               hidden_omega_0=30.0)
+    eng = SirenEngine(model, coords, torch.from_numpy(target), lr=ref["lr0"], min_lr=ref.get("min_lr", 1e-6),
+                      factor=ref.get("factor", 0.8), patience=ref["patience"], hist_cap=ref["steps"], device=dev)
+    t0 = time.perf_counter()
+    eng.step()
+    eng.capture_graph()
+    eng.run(ref["steps"] - 1)
+    torch.cuda.synchronize(dev)
+    fit_s = time.perf_counter() - t0
+    out = eng.infer(coords.to(dev)).cpu().numpy()
+    snr = float(calculate_snr(target, out))
+    losses, lrs = eng.history()
+    return {"snr_target_db": snr, "reference_snr_target_db": run["snr_target"],
+            "delta_db": snr - run["snr_target"], "tolerance_db": 0.1,
+            "steps": ref["steps"], "coords": int(target.size), "lr0": ref["lr0"], "patience": ref["patience"],
+            "final_lr": float(lrs[-1]), "reference_final_lr": float(run["lr"][-1]),
+            "fp16_overflow_steps": eng.guard_state()["overflows"], "fit_seconds": fit_s,
+            "fixture": os.path.relpath(path, ROOT),
+            "workload": f"SIREN {ref['num_sine'] + 1}x{ref['hidden']}, omega0 {ref['omega0']:g}, gt_bach "
+                        f"{target.size} samples, full batch, seed 0: SNR_target of the final weights vs the "
+                        f"reference's run of the same fit (make_golden.py)"}
+
+
 def run_kan(args, world, rank, dev, dist, lib, _lib):
     """cfg5: KAN([1, H, H, 1]) full-batch fit step (KanEngine, siren_kan_train_step)."""
     from inr_for_audio_amd.engine import KanEngine
@@ -319,6 +405,7 @@ def main():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-recon-snr", action="store_true", help="skip the recon-SNR fit (cfg2, N = 1)")
     ap.add_argument("--cpu-coords", type=int, default=65536)
     ap.add_argument("--cpu-steps", type=int, default=6)
     args = ap.parse_args()
@@ -463,6 +550,10 @@ def main():
         "final_loss": loss,
         "fp16_overflow_steps": eng.guard_state()["overflows"],
     }
+    if dist is not None:
+        result["dist"] = dp_report(eng, args, dev, dist)
+    if world == 1 and args.config == "cfg2" and not args.no_recon_snr:
+        result["recon_snr"] = recon_snr(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # BASELINE.md CPU plan: median of steps 2..k with torch.set_num_threads(os.cpu_count()).  On
         # the GPU box os.cpu_count() reports the whole host (256) while the job's CPU share is

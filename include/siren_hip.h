@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SIREN_ABI_VERSION 11
+#define SIREN_ABI_VERSION 12
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 /* ints in one tile-queue counter set (siren_batch.tileq, siren_inner_fwd's tileq): the
@@ -44,6 +44,10 @@ enum siren_status {
 };
 
 int siren_abi_version(void);
+/* ABI 12: hex SHA-256 of the sources this library was compiled from (the .hip and .h files of csrc and this
+ * header) and of its compile defines -- the binding compares it with the sources beside it, so a
+ * stale or foreign library is refused instead of trusted by file time */
+const char* siren_build_id(void);
 /* sizeof of the ABI structs, for binding checks: 0 siren_net, 1 siren_grads, 2 siren_batch,
  * 3 siren_opt_state, 4 siren_kan_net, 5 siren_kan_grads, 6 siren_kan_batch, 7 siren_guard
  * (-1: unknown) */
@@ -69,14 +73,20 @@ typedef struct siren_opt_state {
  * (nothing advances: no step, no history entry), headroom drops by 4, and the caller's next
  * step recomputes the same gradients with a 16x smaller S -- GradScaler-style, but with no
  * optimizer step lost.  After 1000 clean steps headroom grows back by 1 (up to its initial
- * value).  Zero-initialise it and set headroom = 6 (the fixed value used when NULL). */
+ * value).  Zero-initialise it and set headroom = 6 (the fixed value used when NULL).
+ * ABI 12: `stalls` counts hand-off waits of the fused last layer (siren_train_step with
+ * SIREN_OPT_HEAD_FUSE) that gave up because a band partner never published its head partial (a
+ * partner kept off the chip, e.g. CUs held by another process).  Such a step's loss and gradients
+ * are void: while stalls != 0 siren_apply_update skips Adam and the scheduler (no step, no history
+ * entry, headroom untouched) -- the counter is sticky, the caller reads it, reports the failure and
+ * zeroes it before training on. */
 typedef struct siren_guard {
   int32_t flag;        /* this step: non-finite gradients seen (written by apply_update)  */
   int32_t headroom;    /* S exponent target: max|g| max|w_head| omega S < 2^headroom       */
   int32_t clean;       /* consecutive clean steps since the last overflow                   */
   int32_t overflows;   /* steps skipped and recomputed so far                               */
   int32_t headroom0;   /* initial / maximum headroom                                       */
-  int32_t pad0;
+  int32_t stalls;      /* fused last layer: timed-out hand-off waits (sticky; ABI 12)       */
 } siren_guard;
 
 /* ---- one L x H network (SirenWithSnakeTanh, models.py:306-394) ------------------------
@@ -111,7 +121,9 @@ typedef struct siren_grads {
   float* W0; float* b0;
   float* W[SIREN_MAX_INNER]; float* b[SIREN_MAX_INNER];
   float* w_head; float* b_head;
-  float* sse;                               /* [1] sum of squared errors of valid rows */
+  float* sse;                               /* [2] sum of squared errors of valid rows, then (ABI 12)
+                                               the fused hand-off's stall flag: both accumulate like the
+                                               gradients and ride the same all-reduce */
   float* flat; int64_t flat_len;            /* if flat != NULL and zero_grads: memset   */
   float* a[SIREN_MAX_INNER];                /* [H] Snake a gradients (SNAKE layers)     */
   float* a0;                                /* [H] first-layer Snake a (first_snake)    */
@@ -159,7 +171,10 @@ typedef struct siren_batch {
    * taken from those partials; the range guard catches a step whose |g| outgrew it).  0: a Snake
    * last layer runs unfused.  Sine / Tanh last layers ignore it. */
   int32_t head_scale_prev;
-  const siren_guard* guard;  /* range guard (NULL: fixed headroom 6, no overflow recovery) */
+  /* range guard (NULL: fixed headroom 6, no overflow recovery).  ABI 12: not const -- a fused last
+   * layer whose hand-off wait times out counts it in guard->stalls (with no guard it can only turn
+   * the band's loss into NaN) */
+  siren_guard* guard;
   int32_t* tileq;            /* SIREN_TILEQ_INTS ints of tile-queue counters on the device of the
                                 activations (NULL: the forward GEMM's static tile walk) */
 } siren_batch;
@@ -193,6 +208,8 @@ int siren_apply_update(const siren_net* net, float* params, const float* grads_f
                        siren_opt_state* state, const float* sse, double n_total,
                        float* loss_hist, double* lr_hist, int64_t hist_cap,
                        siren_guard* guard /* NULL: no range check */, void* stream);
+/* (siren_apply_update: `sse` is siren_grads.sse after any all-reduce -- sse[1] != 0 marks the guard
+ * stalled, so every rank skips a step any rank's fused hand-off voided) */
 
 /* ---- individual kernels (parity tests call these one by one) ------------------------ */
 /* utils.py:99-109 get_coord: torch.linspace(-1,1,n_total) at [offset, offset+rows) */
@@ -350,7 +367,9 @@ typedef struct siren_kan_grads {
   float* base_w[SIREN_KAN_MAX_LAYERS];
   float* spline_w[SIREN_KAN_MAX_LAYERS];
   float* scaler[SIREN_KAN_MAX_LAYERS];
-  float* sse;                               /* [1] sum of squared errors of valid rows */
+  float* sse;                               /* [2] sum of squared errors of valid rows, then (ABI 12)
+                                               the fused hand-off's stall flag: both accumulate like the
+                                               gradients and ride the same all-reduce */
   float* flat; int64_t flat_len;            /* if flat != NULL and zero_grads: memset   */
 } siren_kan_grads;
 typedef struct siren_kan_batch {
@@ -416,13 +435,18 @@ enum siren_prof_kind {
  * forward modes, 2: in every mode, 0: never (the static walk b, b + G, ...).  Results are
  * identical.  (Options 5 and 7, the round-2 start stagger and X L2-prefetch distance, were
  * measured neutral or slower and retired with their kernels: they return SIREN_ERR_CONFIG.)
+ * SIREN_OPT_HB_FAULT = measurement / test hook of the fused last layer's hand-off, accepted only by
+ *   -DSIREN_DIAG libraries (product: SIREN_ERR_CONFIG for non-zero): bit 0 -- the blocks of column
+ *   tile 1 never publish their head partials; value >> 8 (when non-zero) -- the wait's poll limit
+ *   (default 2^25 polls of s_sleep 1).  Used to drive the timeout branch in tests.
  * SIREN_OPT_HEAD_FUSE = 1 (default): siren_train_step runs a sine last layer on 256x256
  * ping-pong tiles as one launch with the head, the loss gradient and the head backward
  * (dZ_L is written instead of Y_L / C_L; the backward scale S then comes from a bound of
  * max|g| known before the forward); 0: separate forward, head_loss and head_bwd launches. */
 enum siren_option {
   SIREN_OPT_NT_TILE = 0, SIREN_OPT_TN_TILE = 1, SIREN_OPT_NT_PIPE = 2, SIREN_OPT_TN_PIPE = 3,
-  SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_DIAG = 6, SIREN_OPT_NT_QUEUE = 8, SIREN_OPT_HEAD_FUSE = 9
+  SIREN_OPT_NT_GRID = 4, SIREN_OPT_NT_DIAG = 6, SIREN_OPT_NT_QUEUE = 8, SIREN_OPT_HEAD_FUSE = 9,
+  SIREN_OPT_HB_FAULT = 10
 };
 int siren_set_option(int32_t option, int32_t value);
 int siren_profile_enable(int32_t max_records);

@@ -13,7 +13,7 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so the library bin
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 MAX_INNER = 16
 ROW_TILE = 128
 TILEQ_INTS = 768  # SIREN_TILEQ_INTS: one tile-queue counter set
@@ -41,7 +41,7 @@ class SirenOptState(ctypes.Structure):
 class SirenGuard(ctypes.Structure):
     """siren_guard: fp16 backward range guard (include/siren_hip.h)."""
     _fields_ = [("flag", _i32), ("headroom", _i32), ("clean", _i32), ("overflows", _i32),
-                ("headroom0", _i32), ("pad0", _i32)]
+                ("headroom0", _i32), ("stalls", _i32)]
 
 
 HEADROOM0 = 6
@@ -112,6 +112,7 @@ class SirenKanBatch(ctypes.Structure):
 # suite checks that every symbol the header declares is exported.
 _SIGS = {
     "siren_abi_version": (ctypes.c_int, []),
+    "siren_build_id": (ctypes.c_char_p, []),
     "siren_struct_size": (_i64, [_i32]),
     "siren_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "siren_default_splits": (_i32, [_i32, _i32]),
@@ -198,17 +199,25 @@ class SirenError(RuntimeError):
 
 
 def load(path: str = LIB_PATH):
-    """Load (once) and return the native library; raises if it is absent or mismatched."""
+    """Load (once) and return the native library; raises if it is absent or mismatched: wrong ABI,
+    or (when the sources are beside it) a build id that is not the hash of those sources."""
     global _lib
     if _lib is not None:
         return _lib
-    _lib = bind(path)
+    _lib = bind(path, expect_build_id=expected_build_id())
     return _lib
 
 
-def bind(path: str):
+def expected_build_id(defines=()) -> str | None:
+    """buildinfo.source_hash of the sources in this tree (None when they are not shipped)."""
+    from . import buildinfo
+    return buildinfo.source_hash(defines) if buildinfo.sources_present() else None
+
+
+def bind(path: str, expect_build_id: str | None = None):
     """A freshly bound (uncached) handle of the library at `path`: tools/ab_bench.py loads the
-    product library beside measurement builds of it under other file names."""
+    product library beside measurement builds of it under other file names.  expect_build_id: refuse
+    a library compiled from other sources (siren_build_id, include/siren_hip.h)."""
     if not os.path.exists(path):
         raise SirenError(
             f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
@@ -220,6 +229,9 @@ def bind(path: str):
         fn.argtypes = args
     if lib.siren_abi_version() != ABI_VERSION:
         raise SirenError(f"libsiren_hip ABI {lib.siren_abi_version()} != expected {ABI_VERSION}")
+    if expect_build_id is not None and lib.siren_build_id().decode() != expect_build_id:
+        raise SirenError(f"{path} was built from other sources (build id {lib.siren_build_id().decode()[:12]}, "
+                         f"sources {expect_build_id[:12]}): rebuild with __graft_entry__.build()")
     for k, st in enumerate(STRUCTS):
         if lib.siren_struct_size(k) != ctypes.sizeof(st):
             raise SirenError(f"{st.__name__}: ctypes size {ctypes.sizeof(st)} != C size {lib.siren_struct_size(k)}")

@@ -175,6 +175,7 @@ hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s, bool h
       p.n_valid = b->n_valid; p.loss_mode = b->loss_mode; p.gfac = gfac; p.head_omega = n->head_omega;
       p.gscale = b->gscale; p.dZ = B(b->dZ[0]); p.colsum_part = b->col_part;
       p.gmax_part = b->gmax_part;  // this launch's max|g|: the next one's scale (Snake last layer)
+      p.stall = b->guard ? &((GuardState*)b->guard)->stalls : nullptr;  // a timed-out hand-off voids the step
       close_run();
       SIREN_PROF(SIREN_PROF_HEAD_FWD, s, gemm_nt(hb_mode(n->act[i]), true, p, s));
       continue;
@@ -196,6 +197,14 @@ hipError_t run_forward(const siren_net* n, siren_batch* b, hipStream_t s, bool h
 extern "C" {
 
 int siren_abi_version(void) { return SIREN_ABI_VERSION; }
+
+// __graft_entry__._compile passes the hash of the sources and defines; the marker prefix lets the
+// build step read it from the file without loading the library
+#ifndef SIREN_BUILD_ID
+#define SIREN_BUILD_ID "unknown"
+#endif
+static const char kBuildId[] = "SIREN_BUILD_ID=" SIREN_BUILD_ID;
+const char* siren_build_id(void) { return kBuildId + 15; }
 
 int64_t siren_struct_size(int32_t which) {
   switch (which) {
@@ -392,7 +401,10 @@ int siren_train_step(const siren_net* net, const siren_grads* gr, siren_batch* b
                                              b->target, b->n_valid, gfac, b->out, b->g, b->sse_part,
                                              b->gsum_part, b->gmax_part, s, net->head_omega, b->loss_mode));
   const int nsum = (R + 255) / 256;
-  SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to2(b->sse_part, gr->sse, b->gsum_part, gr->b_head, nsum, 1, s));
+  // sse[1]: the fused hand-off's stall flag rides the gradient all-reduce with the sse (siren_grads.sse)
+  const int* stall = (hb && b->guard) ? &((const GuardState*)b->guard)->stalls : nullptr;
+  SIREN_PROF(SIREN_PROF_REDUCE, s, sum_to2(b->sse_part, gr->sse, b->gsum_part, gr->b_head, nsum, 1, s, stall,
+                                           gr->sse + 1));
   // ---- backward (autograd of run.py:185) ----
   return run_backward(net, gr, b, s, hb);
 }
@@ -434,7 +446,7 @@ int siren_apply_update(const siren_net* net, float* params, const float* grads_f
     cs.WTb[i] = B(WTh[i]);
   }
   GuardState* gd = (GuardState*)guard;
-  if (gd) SIREN_PROF(SIREN_PROF_UPDATE, s, guard_check(grads_flat, n_params, gd, s));
+  if (gd) SIREN_PROF(SIREN_PROF_UPDATE, s, guard_check(grads_flat, n_params, gd, s, sse));
   SIREN_PROF(SIREN_PROF_UPDATE, s, adam_flat(params, grads_flat, exp_avg, exp_avg_sq, n_params,
                                              (const OptState*)state, s, gd, sse));
   SIREN_PROF(SIREN_PROF_UPDATE, s, cast_weights(cs, net->hidden, s));
@@ -744,6 +756,8 @@ int siren_set_option(int32_t option, int32_t value) {
       if (value < 0 || value > 1) return SIREN_ERR_CONFIG;
       g_head_fuse = value;
       return SIREN_OK;
+    case SIREN_OPT_HB_FAULT:
+      return (value >= 0 && gemm_nt_set_hb_fault(value)) ? SIREN_OK : SIREN_ERR_CONFIG;
   }
   return SIREN_ERR_CONFIG;
 }

@@ -507,20 +507,29 @@ hipError_t sum_to(const float* x, int n, float* out, int accumulate, hipStream_t
   return hipGetLastError();
 }
 
-// two independent sum_to in one launch (block z: x_z -> out_z), each in sum_to's order
+// two independent sum_to in one launch (block z: x_z -> out_z), each in sum_to's order; with
+// flag_src, block 0 also adds (flag_src[0] != 0) to flag_dst[0] (the stall slot beside the sse)
 __global__ void sum_to2_kernel(const float* __restrict__ x0, float* out0, const float* __restrict__ x1, float* out1,
-                               int n, int accumulate) {
+                               int n, int accumulate, const int* __restrict__ flag_src, float* flag_dst) {
   __shared__ float scratch[16];
   const float* x = blockIdx.x ? x1 : x0;
   float* out = blockIdx.x ? out1 : out0;
   float s = 0.f;
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[i];
   s = block_sum(s, scratch);
-  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + s : s;
+  if (threadIdx.x == 0) {
+    out[0] = accumulate ? out[0] + s : s;
+    if (blockIdx.x == 0 && flag_src) {
+      const float f = flag_src[0] != 0 ? 1.0f : 0.0f;
+      flag_dst[0] = accumulate ? flag_dst[0] + f : f;
+    }
+  }
 }
 
-hipError_t sum_to2(const float* x0, float* out0, const float* x1, float* out1, int n, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(sum_to2_kernel, dim3(2), dim3(1024), 0, s, x0, out0, x1, out1, n, accumulate);
+hipError_t sum_to2(const float* x0, float* out0, const float* x1, float* out1, int n, int accumulate, hipStream_t s,
+                   const int* flag_src, float* flag_dst) {
+  hipLaunchKernelGGL(sum_to2_kernel, dim3(2), dim3(1024), 0, s, x0, out0, x1, out1, n, accumulate, flag_src,
+                     flag_dst);
   return hipGetLastError();
 }
 
@@ -532,7 +541,7 @@ hipError_t sum_to2(const float* x0, float* out0, const float* x1, float* out1, i
 //   d = sqrt(v) / sqrt(bc2) + eps              (correctly rounded sqrt/div)
 //   p = p + ((-lr/bc1) * m) / d                (addcdiv_)
 // bias corrections in fp64 from the device step counter.  A step the range guard rejects
-// (guard_skip) leaves p, m, v untouched.
+// (guard_skip: an fp16 overflow, or a fused hand-off that timed out) leaves p, m, v untouched.
 __global__ void adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
                                  float* __restrict__ m, float* __restrict__ v, int64_t n,
                                  const OptState* __restrict__ st, const GuardState* __restrict__ guard,
@@ -571,20 +580,25 @@ hipError_t adam_flat(float* p, const float* g, float* m, float* v, int64_t n, co
 
 // ---------------------------------------------------------------------------------
 // Range guard check (siren_apply_update, before Adam): guard->flag |= any non-finite value
-// in the reduced gradient vector g[0..n).  One atomic per block that found one.
-__global__ void guard_check_kernel(const float* __restrict__ g, int64_t n, GuardState* guard) {
+// in the reduced gradient vector g[0..n).  One atomic per block that found one.  sse[1] (the
+// reduced stall slot: non-zero when any micro-batch on any rank had a fused hand-off time out)
+// marks the guard stalled, so every data-parallel rank skips the voided step, not only the one
+// whose wait gave up.
+__global__ void guard_check_kernel(const float* __restrict__ g, int64_t n, GuardState* guard,
+                                   const float* __restrict__ sse) {
   __shared__ float scratch[4];
   float bad = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     if (!__builtin_isfinite(g[i])) bad = 1.f;
   bad = block_max(bad, scratch);
   if (threadIdx.x == 0 && bad > 0.f) atomicOr(&guard->flag, 1);
+  if (threadIdx.x == 0 && blockIdx.x == 0 && sse && sse[1] != 0.f) atomicMax(&guard->stalls, 1);
 }
 
-hipError_t guard_check(const float* g, int64_t n, GuardState* guard, hipStream_t s) {
+hipError_t guard_check(const float* g, int64_t n, GuardState* guard, hipStream_t s, const float* sse) {
   hipError_t e = hipMemsetAsync(&guard->flag, 0, sizeof(int32_t), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(guard_check_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, s, g, n, guard);
+  hipLaunchKernelGGL(guard_check_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, s, g, n, guard, sse);
   return hipGetLastError();
 }
 
@@ -600,7 +614,9 @@ __global__ void plateau_kernel(OptState* st, const float* sse, double n_total, f
                                double* lr_hist, int64_t hist_cap, GuardState* guard) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   if (guard) {
-    if (guard_skip(guard, sse)) {
+    // a voided step (fused hand-off timeout): nothing advances, and the headroom is not to blame
+    if (guard_stalled(guard)) return;
+    if (guard_overflow(guard, sse)) {
       guard->headroom -= kHeadroomDrop;
       guard->clean = 0;
       guard->overflows += 1;

@@ -143,7 +143,9 @@ __device__ __forceinline__ float tanh_epi(float x) {
 // NT_FWD_HB: head_part word not yet published by its column tile's block (launch_nt fills it)
 constexpr unsigned kHeadPending = 0xFFFFFFFFu;
 // polls (s_sleep 1 = 64 clocks each, ~1-1.4 s in all) before a hand-off wait gives up; a partner
-// normally publishes within one tile period (~40 us)
+// normally publishes within one tile period (~40 us).  A wait that gives up is counted in the
+// range guard's stall word (NtParams::stall -> GuardState::stalls), which voids the step: the
+// update kernels skip it and the engine raises (include/siren_hip.h siren_guard)
 constexpr int kHeadSpinLimit = 1 << 25;
 
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
@@ -427,8 +429,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         for (int w = 0; w < WN; ++w) own += red[w * BM + tid];
         const int m = m0 + tid;
         unsigned* hpu = (unsigned*)p.head_part;
-        __hip_atomic_store(hpu + (size_t)tn * p.M + m, own == own ? __float_as_uint(own) : 0x7fc00000u,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // SIREN_OPT_HB_FAULT bit 0 (SIREN_DIAG builds): column tile 1 never publishes (test hook)
+        if (!(SIREN_DIAG_ON && (p.hb_fault & 1) && tn == 1))
+          __hip_atomic_store(hpu + (size_t)tn * p.M + m, own == own ? __float_as_uint(own) : 0x7fc00000u,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         float o = 0.f;  // head_loss_kernel's order: partials j = 0, 1, ..., then the bias
         for (int jt = 0; jt < tiles_n; ++jt) {
           float v = own;
@@ -437,10 +441,13 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             int polls = 0;
             while ((u = __hip_atomic_load(hpu + (size_t)jt * p.M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
                    kHeadPending) {
-              // bounded: a partner kept off the chip (CUs held by another process) turns the band's
-              // loss into NaN -- a loud failure of the step -- instead of hanging the launch
-              if (++polls > kHeadSpinLimit) {
+              // bounded: a partner kept off the chip (CUs held by another process) voids the step
+              // instead of hanging the launch -- the band's partial becomes NaN and the wait is
+              // counted in the guard's stall word, which makes the update skip the step and the
+              // engine raise (a NaN alone would pass guard_skip and reach the weights)
+              if (++polls > p.spin_limit) {
                 u = 0x7fc00000u;
+                if (p.stall) __hip_atomic_fetch_add(p.stall, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
               }
               __builtin_amdgcn_s_sleep(1);
@@ -1010,6 +1017,12 @@ bool gemm_nt_set_diag(int bits) {
 }
 static int g_nt_queue = 1;  // 0 off, 1 forward modes, 2 every ping-pong mode
 void gemm_nt_set_queue(int v) { g_nt_queue = v; }
+static int g_hb_fault = 0;  // SIREN_OPT_HB_FAULT (SIREN_DIAG builds)
+bool gemm_nt_set_hb_fault(int v) {
+  if (!SIREN_DIAG_ON && v) return false;  // product builds carry no fault injection
+  g_hb_fault = v;
+  return true;
+}
 
 // CU count of the stream's device (queried once per device)
 static int stream_cus(hipStream_t s) {
@@ -1060,6 +1073,8 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
     else g -= g % tiles_n;
     if (g < tiles_n) g = tiles_n;
     if (!hb_coresident(MODE, g, s)) return hipErrorCooperativeLaunchTooLarge;
+    p.hb_fault = g_hb_fault & 0xff;
+    p.spin_limit = (g_hb_fault >> 8) > 0 ? (g_hb_fault >> 8) : kHeadSpinLimit;
     const hipError_t e = hipMemsetAsync(p.head_part, 0xFF, (size_t)tiles_n * p.M * sizeof(float), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD>), dim3(g), dim3(Cfg::THREADS), 0, s, p);

@@ -21,8 +21,14 @@ constexpr float kInvPi = 0.31830988618379067f;   // 1/pi, rounded to fp32
 
 // Snake y = z + sin^2(a z)/a (models.py:241) with dY/dz = 1 + sin(2az) and dY/da =
 // (z sin(2az) - sin^2(az)/a)/a, from the double angle: sin^2(az) = (1 - cos 2az)/2, so one
-// sin / cos pair of 2az (in revolutions) and 7 other VALU, where the single-angle form takes 11.
-// Same absolute error (the fp16 outputs and the fp32 argument bound it); ia = 1/a.
+// sin / cos pair of 2az (in revolutions) and 7 other VALU, where the single-angle form takes 11;
+// ia = 1/a.  Error: away from small |az| the fp16 outputs and the fp32 argument bound it, as for the
+// single angle.  For small |az|, 1 - cos 2az cancels (cos -> 1): t = sin^2(az)/a carries the
+// absolute error of the hardware cos near 1 (~2^-24) over 2a, and E = (z s - t)/a that over a
+// again -- ~1e-7 ABSOLUTE at a = 0.5 where E ~ z^2 is tiny (relative error then grows as z -> 0),
+// where the single angle's t = s^2/a would keep E relatively exact.  That is about two fp16
+// subnormal steps (2^-24 = 6e-8 is the fp16 output's own resolution near 0), so the double angle
+// stays; tests/test_gpu_act.py::test_snake_small_az_error bounds it against fp64.
 __device__ __forceinline__ void snake_epi(float z, float a, float ia, float& y, float& d, float& e) {
   const float x = __builtin_amdgcn_fractf((z * a) * kInvPi);  // 2 a z in revolutions
   const float s = __builtin_amdgcn_sinf(x), c = __builtin_amdgcn_cosf(x);

@@ -65,6 +65,10 @@ struct NtParams {
   int n_valid, loss_mode;
   float gfac, head_omega;
   float* gmax_part;     // [M/256] max|g| per band (NT_FWD_HB*; null = not written)
+  // NT_FWD_HB*: a hand-off wait that gives up (spin_limit polls) adds 1 here (GuardState::stalls;
+  // null = only the NaN partial); hb_fault: SIREN_OPT_HB_FAULT injection (SIREN_DIAG builds only)
+  int* stall;
+  int spin_limit, hb_fault;
 };
 constexpr int kTileqInts = 768;  // == SIREN_TILEQ_INTS (include/siren_hip.h)
 
@@ -80,6 +84,7 @@ void gemm_tn_set_pipe(int v);     // 256x256 K-loop variant (TnL0..TnL2)
 void gemm_nt_set_grid_cap(int cap);  // persistent grid size override (0 = #CUs)
 bool gemm_nt_set_diag(int bits);     // SIREN_OPT_NT_DIAG (false: not a SIREN_DIAG build)
 void gemm_nt_set_queue(int on);       // SIREN_OPT_NT_QUEUE: dynamic tile queue (ping-pong K-loop)
+bool gemm_nt_set_hb_fault(int v);     // SIREN_OPT_HB_FAULT (false: not a SIREN_DIAG build)
 struct TnParams {
   const h16* Y;   // [R][Hin]   layer input (A role: dW column index k)
   const h16* dZ;  // [R][Hout]  layer pre-activation gradient (B role: dW row index o)
@@ -102,7 +107,8 @@ hipError_t coords_fill_grid(float* xy, int64_t rows, int64_t offset, int64_t hei
 
 // fp16 backward range guard (include/siren_hip.h siren_guard)
 struct GuardState {
-  int32_t flag, headroom, clean, overflows, headroom0, pad0;
+  int32_t flag, headroom, clean, overflows, headroom0;
+  int32_t stalls;  // fused last layer: timed-out hand-off waits (sticky; the host clears it)
 };
 constexpr int kHeadroomDefault = 6;      // grad_scale target exponent without a guard
 constexpr int kHeadroomDrop = 4;         // per rejected step (S / 16)
@@ -110,10 +116,17 @@ constexpr int kHeadroomMin = -14;        // below this a non-finite gradient is 
 constexpr int kHeadroomGrowAfter = 1000; // clean steps before headroom grows back by one
 // true when the step's gradients hold a non-finite value, the loss is finite (so it is the
 // fp16 dZ storage that overflowed, not a diverged fit) and the headroom can still drop
-__device__ __forceinline__ bool guard_skip(const GuardState* g, const float* sse) {
+__device__ __forceinline__ bool guard_overflow(const GuardState* g, const float* sse) {
   return g && g->flag && __builtin_isfinite(sse[0]) && g->headroom > kHeadroomMin;
 }
-hipError_t guard_check(const float* g, int64_t n, GuardState* guard, hipStream_t s);
+// a fused last layer's hand-off timed out: the step's loss and gradients are void
+__device__ __forceinline__ bool guard_stalled(const GuardState* g) { return g && g->stalls != 0; }
+// the update is skipped (Adam leaves p, m, v untouched; the scheduler does not step)
+__device__ __forceinline__ bool guard_skip(const GuardState* g, const float* sse) {
+  return guard_stalled(g) || guard_overflow(g, sse);
+}
+// sse (nullable): the reduced [sse, stall slot] pair of siren_grads (a non-zero stall slot marks the guard stalled)
+hipError_t guard_check(const float* g, int64_t n, GuardState* guard, hipStream_t s, const float* sse = nullptr);
 // a0 / E0 non-null: Linear + Snake first layer (first_linear=True); C0 null: Y0 only
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
                      int R, int H, h16* Y0, h16* C0, hipStream_t s, const float* a0 = nullptr,
@@ -216,7 +229,9 @@ struct CastSet {
 };
 hipError_t cast_weights(const CastSet& cs, int H, hipStream_t s);
 hipError_t sum_to(const float* x, int n, float* out, int accumulate, hipStream_t s);
-// sum_to(x0 -> out0) and sum_to(x1 -> out1) in one launch
-hipError_t sum_to2(const float* x0, float* out0, const float* x1, float* out1, int n, int accumulate, hipStream_t s);
+// sum_to(x0 -> out0) and sum_to(x1 -> out1) in one launch; flag_src non-null: also
+// flag_dst[0] (+)= (flag_src[0] != 0)
+hipError_t sum_to2(const float* x0, float* out0, const float* x1, float* out1, int n, int accumulate, hipStream_t s,
+                   const int* flag_src = nullptr, float* flag_dst = nullptr);
 
 }  // namespace siren

@@ -231,7 +231,8 @@ LOSS_MODES = {"mse": 0, "mae": 1}   # run.py:161-169 (MSELoss / L1Loss)
 
 
 def new_guard(device) -> torch.Tensor:
-    """A zeroed siren_guard with the default headroom (include/siren_hip.h)."""
+    """A zeroed siren_guard with the default headroom (include/siren_hip.h): flag, headroom, clean,
+    overflows, headroom0, stalls."""
     g = torch.zeros(6, dtype=torch.int32)
     g[1] = g[4] = _lib.HEADROOM0
     return g.to(device)
@@ -257,6 +258,9 @@ class SirenEngine:
     (siren_batch.grad_ready events), so RCCL runs under the remaining backward GEMMs."""
 
     _buckets = None  # [(event index, lo, hi)] in completion order (DP only)
+    # bench.py's exposed-communication measurement only: False skips the gradient all-reduce (the
+    # ranks' parameters then drift apart -- timing passes after the measured run, never training)
+    comm_enabled = True
 
     def __init__(self, model, coords: torch.Tensor, target: torch.Tensor, *, lr: float = 1e-3,
                  min_lr: float = 1e-6, factor: float = 0.8, patience: int = 200,
@@ -339,12 +343,20 @@ class SirenEngine:
         self.ws = Workspace(spec, mb, dev, train=True, splits=splits)
         self.guard = new_guard(dev)
         self.batches = []
+        # max|g| partials per micro-batch: a fused Snake last layer takes its backward scale from the
+        # partials of the previous launch over the SAME rows (siren_batch.head_scale_prev), i.e. this
+        # micro-batch's in the previous step -- with one shared slice it would be the previous
+        # micro-batch's, and a quiet segment after a loud one would drop its dZ into fp16 subnormals
+        nsum = (mb + 255) // 256
+        self._gmax = torch.zeros(self.n_micro, nsum, dtype=torch.float32, device=dev)
         for k in range(self.n_micro):
             lo = k * mb
             c = self.coords[lo:lo + mb]
             t = self.target[lo:lo + mb]
-            self.batches.append(self.ws.batch(c, t, min(mb, n - lo), n_global, zero_grads=(k == 0),
-                                              guard=self.guard, loss_mode=LOSS_MODES[loss_mode]))
+            b = self.ws.batch(c, t, min(mb, n - lo), n_global, zero_grads=(k == 0),
+                              guard=self.guard, loss_mode=LOSS_MODES[loss_mode])
+            b.gmax_part = ptr(self._gmax[k])
+            self.batches.append(b)
         self.steps_done = 0
         self.graph = None
         if d is not None:
@@ -386,11 +398,13 @@ class SirenEngine:
         for b in self.batches:
             check(self.lib.siren_train_step(ctypes.byref(self.net), ctypes.byref(self.grad_struct),
                                             ctypes.byref(b), s), "siren_train_step")
-        # the workspace's gmax_part now holds a launch's max|g| partials: from the next step on a
-        # Snake last layer may run fused with the head, its backward scale taken from them
-        # (include/siren_hip.h siren_batch.head_scale_prev)
-        for b in self.batches:
-            b.head_scale_prev = 1
+        # every micro-batch's gmax_part now holds its launch's max|g| partials: from the next step on
+        # a Snake last layer may run fused with the head, its backward scale taken from them
+        # (include/siren_hip.h siren_batch.head_scale_prev).  Not while capturing a graph: nothing
+        # has run, and the graph would record the unfused launch for good (capture_graph)
+        if not torch.cuda.is_current_stream_capturing():
+            for b in self.batches:
+                b.head_scale_prev = 1
 
     def _launch_update(self):
         check(self.lib.siren_apply_update(
@@ -407,7 +421,7 @@ class SirenEngine:
             self.graph.replay()
         else:
             self._launch_grads()
-            d = _dist()
+            d = _dist() if self.comm_enabled else None
             if d is not None and self._buckets is not None:
                 # bucket k goes out as soon as the backward recorded grad_ready[k]
                 works = []
@@ -424,11 +438,21 @@ class SirenEngine:
         self.steps_done += 1
 
     def capture_graph(self, warmup: int = 0):
-        """Capture one whole step as a HIP graph (single-process only)."""
+        """Capture one whole step as a HIP graph (single-process only).
+
+        The graph replays the launch configuration of the capture.  A stack whose last inner layer
+        is a Snake runs that layer fused with the head only once a step has run (its backward scale
+        comes from the previous launch's max|g|), so capturing before any step records the unfused
+        launches for the whole run: run one step first (warmup >= 1, or step() as run.train does);
+        this case warns."""
         if _dist() is not None:
             raise RuntimeError("graph capture is for the single-GPU path")
         for _ in range(warmup):
             self.step()
+        if self.steps_done == 0 and self.spec.act(self.spec.n_inner - 1) == _lib.ACT_SNAKE:
+            import warnings
+            warnings.warn("capture_graph before any step: the Snake last layer is captured unfused "
+                          "(run one step first to capture the fused launch)", RuntimeWarning, stacklevel=2)
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.device)
@@ -446,15 +470,30 @@ class SirenEngine:
 
     def steps_applied(self) -> int:
         """Optimizer steps taken by this engine (scheduler steps of this run); step() calls
-        minus the ones the fp16 range guard rejected and recomputed (synchronises)."""
+        minus the ones the fp16 range guard rejected and recomputed (synchronises).  Raises
+        SirenError if a fused last layer's hand-off timed out since the last clear_stalls()."""
+        self.guard_state()
         return int(self.opt_state().last_epoch)
 
     def guard_state(self) -> dict:
-        """{'headroom', 'overflows', 'clean'} of the fp16 backward range guard (synchronises)."""
+        """{'headroom', 'overflows', 'clean', 'stalls'} of the fp16 backward range guard
+        (synchronises).  Raises SirenError when `stalls` is non-zero: a fused last layer's band
+        hand-off gave up waiting for a partner (include/siren_hip.h siren_guard), so that step's
+        loss and gradients were void and its update was skipped -- parameters and optimizer state
+        are those of before it.  clear_stalls() re-arms the guard."""
         if getattr(self, "guard", None) is None:
-            return {"headroom": None, "overflows": 0, "clean": 0}
+            return {"headroom": None, "overflows": 0, "clean": 0, "stalls": 0}
         g = self.guard.cpu().tolist()
-        return {"headroom": g[1], "overflows": g[3], "clean": g[2]}
+        if g[5]:
+            raise _lib.SirenError(
+                f"fused last layer: {g[5]} hand-off wait(s) timed out (a band partner never published its "
+                "head partial -- CUs held by other work?); the step was voided and not applied. "
+                "Call clear_stalls() to train on, or set SIREN_OPT_HEAD_FUSE 0")
+        return {"headroom": g[1], "overflows": g[3], "clean": g[2], "stalls": g[5]}
+
+    def clear_stalls(self) -> None:
+        """Zero the guard's hand-off stall counter (after guard_state() raised)."""
+        self.guard[5] = 0
 
     def run(self, steps: int) -> None:
         """`steps` optimizer steps: step() calls, plus one more for each step the fp16 range

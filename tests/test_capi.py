@@ -44,7 +44,7 @@ def test_struct_layouts_match(lib):
 
 
 def test_host_only_helpers(lib):
-    assert lib.siren_abi_version() == 11
+    assert lib.siren_abi_version() == 12
     assert lib.siren_status_string(0) == b"ok"
     assert b"shape" in lib.siren_status_string(1001)
     assert lib.siren_dw_tile(1 << 20, 1024) == 256 and lib.siren_nt_tile(1 << 20, 1024) == 256
@@ -111,12 +111,12 @@ def test_set_option_ranges(lib):
     the defaults restored; SIREN_OPT_NT_QUEUE takes 0 (static walk), 1 (forward modes), 2 (all).
     The product library carries no measurement ablation: SIREN_OPT_NT_DIAG accepts only 0, and
     the retired stagger (5) and prefetch-distance (7) options are rejected; SIREN_OPT_HEAD_FUSE (9)
-    takes 0 or 1."""
+    takes 0 or 1; the hand-off fault hook SIREN_OPT_HB_FAULT (10) only 0."""
     bad = 1003  # SIREN_ERR_CONFIG
     for opt, good, wrong in ((0, (0, 128, 256), (64,)), (1, (0, 128, 256), (512,)), (2, (-1, 0, 1, 4), (2, 3, 5, 7, -2)),
                              (3, (-1, 4), (5,)), (4, (0, 16), (-1,)), (5, (), (0, 1)),
                              (6, (0,), (1, 4, 512, 1024, 2, 8)), (7, (), (1, 2)), (8, (0, 1, 2), (3, -1)),
-                             (9, (0, 1), (2, -1))):
+                             (9, (0, 1), (2, -1)), (10, (0,), (1, 1 << 8, -1))):
         for v in good:
             assert lib.siren_set_option(opt, v) == 0, (opt, v)
         for v in wrong:
@@ -124,3 +124,40 @@ def test_set_option_ranges(lib):
     assert lib.siren_set_option(99, 0) == bad
     for opt, v in ((0, 0), (1, 0), (2, -1), (3, -1), (4, 0), (6, 0), (8, 1), (9, 1)):
         assert lib.siren_set_option(opt, v) == 0
+
+
+def test_build_id_is_the_source_hash(lib):
+    """The library embeds the SHA-256 of the sources it was compiled from (siren_build_id); the build
+    step reads it from the file and rebuilds on a mismatch, and _lib.load() refuses a library whose
+    id is not the hash of the sources beside it (no file times involved)."""
+    import __graft_entry__ as ge
+    from inr_for_audio_amd import _lib, buildinfo
+    bid = lib.siren_build_id().decode()
+    assert re.fullmatch(r"[0-9a-f]{64}", bid)
+    assert bid == buildinfo.source_hash() == buildinfo.lib_build_id(ge.LIB)
+    assert not ge._stale()
+    # the SIREN_DIAG test library: its own defines, its own id
+    diag = buildinfo.lib_build_id(ge.DIAG_LIB)
+    assert diag == buildinfo.source_hash(ge.DIAG_DEFINES) != bid
+    assert _lib.bind(ge.DIAG_LIB, expect_build_id=diag).siren_build_id().decode() == diag
+    with pytest.raises(_lib.SirenError, match="other sources"):
+        _lib.bind(ge.LIB, expect_build_id="0" * 64)
+    # a one-byte change of any source changes the hash
+    src = os.path.join(buildinfo.CSRC, "gemm_nt.hip")
+    data = open(src, "rb").read()
+    try:
+        open(src, "wb").write(data + b"\n")
+        assert buildinfo.source_hash() != bid and ge._stale()
+    finally:
+        open(src, "wb").write(data)
+    assert buildinfo.source_hash() == bid
+
+
+def test_diag_library_accepts_the_fault_hook():
+    """-DSIREN_DIAG builds take SIREN_OPT_HB_FAULT (the product refuses it: test_set_option_ranges)."""
+    import __graft_entry__ as ge
+    from inr_for_audio_amd import _lib
+    d = _lib.bind(ge.DIAG_LIB)
+    for v in (1, (64 << 8) | 1, 0):
+        assert d.siren_set_option(10, v) == 0, v
+    assert d.siren_set_option(10, -1) == 1003

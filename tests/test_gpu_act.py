@@ -130,6 +130,35 @@ def test_inner_fwd_act(lib, dev, tile, act, R, H, amag, head):
         assert np.max(np.abs(got - ref)) < 1e-4 * max(1.0, np.max(np.abs(ref)))
 
 
+def test_snake_small_az_error(lib, dev):
+    """The Snake epilogue's double angle (siren_common.h snake_epi: sin^2(az) = (1 - cos 2az)/2) cancels
+    for small |az|: t = sin^2(az)/a carries the absolute error of the hardware cos near 1 (~2^-24)
+    over 2a, and E = dY/da = (z sin 2az - t)/a that over a again -- an ABSOLUTE error of ~1e-7 at the
+    default a = 0.5 where E ~ z^2 is tiny, not a relative one.  Bounded here at small
+    |z| against fp64: |E - E_ref| <= one fp16 rounding of E_ref + 4 * 2^-24 / a^2 (+ the fp32 z);
+    Y and D stay within one fp16 rounding plus fp32 slack."""
+    rng = np.random.default_rng(5)
+    R, H = 512, 256
+    X = orc.f16_round(rng.uniform(-1, 1, (R, H)).astype(F32))
+    W = orc.f16_round(rng.uniform(-1, 1, (H, H)).astype(F32) * 2e-4)   # |z| <~ 1e-2
+    b = rng.uniform(-1e-3, 1e-3, H).astype(F32)
+    a = np.full(H, 0.5, F32)
+    Y = torch.empty(R, H, dtype=H16, device=dev)
+    C, E = torch.empty_like(Y), torch.empty_like(Y)
+    ok(lib.siren_inner_fwd_act(ptr(to_dev(X, dev, H16)), ptr(to_dev(W, dev, H16)), ptr(to_dev(b, dev)), SNAKE,
+                               ctypes.c_float(30.0), ptr(to_dev(a, dev)), R, H, ptr(Y), ptr(C), ptr(E), None, None,
+                               ptr(new_tileq(dev)), S()), lib)
+    z = X.astype(np.float64) @ W.astype(np.float64).T + b
+    y, d, e = _snake_ref(z, a.astype(np.float64))
+    eabs = 4.0 * 2.0 ** -24 / 0.25
+    err_e = np.abs(f16_np(E) - e)
+    log("snake_small_az", max_abs_z=float(np.abs(z).max()), max_abs_e=float(np.abs(e).max()),
+        max_err_e=float(err_e.max()), bound_abs=eabs)
+    assert within_f16(f16_np(E), e, eabs) <= 0
+    assert within_f16(f16_np(Y), y, 1e-7) <= 0
+    assert within_f16(f16_np(C), d, 1e-7) <= 0
+
+
 @pytest.mark.parametrize("act", [SNAKE, TANH])
 @pytest.mark.parametrize("R,H,k", [(512, 256, None), (512, 512, 9), (256, 1024, 3)])
 def test_inner_bwd_dx_act(lib, dev, tile, act, R, H, k):

@@ -50,7 +50,27 @@ def test_torchrun_two_ranks_gloo():
                 "--layers", "3", "--no-cpu-baseline"])
     _common(res, 2, "cfg2")
     assert res["config"]["global_batch"] == 2 * 65536 and res["config"]["backend"] == "gloo"
-    assert "cpu_baseline" not in res
+    assert "cpu_baseline" not in res and "recon_snr" not in res
+    # what the process group saw, and how much of the all-reduce the backward hid
+    d = res["dist"]
+    assert d["backend"] == "gloo" and d["world_size_seen"] == 2 and d["rccl"] is False
+    assert d["bucketed_overlap"] is True and d["buckets"] == 2 + 2  # head, 2 inner layers, first layer
+    assert d["ms_per_step_with_allreduce"] > 0 and d["ms_per_step_without_allreduce"] > 0
+    assert d["allreduce_alone_ms"] > 0
+    assert abs(d["exposed_allreduce_ms_per_step"]
+               - (d["ms_per_step_with_allreduce"] - d["ms_per_step_without_allreduce"])) < 1e-9
+
+
+def test_single_gpu_line_carries_recon_snr():
+    """The default line carries both halves of BASELINE's metric: coord-samples/s and, outside the
+    timed region, the recon SNR of the headline model's fit against the reference's run of it."""
+    res = _run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--coords", "65536",
+                "--no-cpu-baseline"])
+    r = res["recon_snr"]
+    assert r is not None and r["fixture"].startswith("tests/golden/")
+    assert abs(r["snr_target_db"] - r["reference_snr_target_db"]) < r["tolerance_db"], r
+    assert r["fp16_overflow_steps"] == 0 and r["final_lr"] == r["reference_final_lr"]
+    assert "dist" not in res
 
 
 def test_torchrun_two_ranks_strong_scaling():

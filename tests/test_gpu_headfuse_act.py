@@ -208,3 +208,63 @@ def test_fused_act_training_graph_and_determinism(dev, opts):
     lb, _ = b.history()
     assert np.array_equal(la, lb)
     assert a.guard_state()["overflows"] == 0
+
+
+def test_snake_head_scale_per_micro_batch(dev, lib, opts):
+    """A fused Snake last layer takes its backward scale S from the max|g| partials of the previous
+    launch over the SAME rows (siren_batch.head_scale_prev): each micro-batch has its own partials
+    (engine._gmax), not the workspace's one slice.  Micro-batches of very different
+    loudness -- a quiet segment, a loud one, a quiet one, in the order a long clip would give them --
+    then each keep the unfused path's scale: no fp16 overflow is ever caught, and the fused step's
+    gradients match the unfused step's at the same weights.  (With one shared slice the loud
+    micro-batch would run on the quiet one's S, ~2^11 too large, and the quiet one after it on the
+    loud one's; the same engine with its batches pointed at one slice is run beside it and its
+    overflow count and gradient error are logged.)"""
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    opts(OPT_NT_TILE, 256)
+    torch.manual_seed(0)
+    H, mb, n = 1024, 4096, 12288
+    model = SirenWithSnakeTanh(1, 1, H, 1, 1, 0, first_omega_0=3000.0, hidden_omega_0=30.0, a_initial=0.5)
+    t = torch.linspace(-1, 1, n).reshape(n, 1)
+    amp = torch.ones(n)
+    amp[mb:2 * mb] = 2000.0  # the loud segment: |g| ~ 10^3 x the quiet ones'
+    y = amp * (0.5 * torch.sin(37 * t[:, 0]) + 0.3 * torch.sin(91 * t[:, 0] + 0.5))
+    eng = SirenEngine(model, t, y, micro_batch=mb, device=dev)
+    assert eng.n_micro == 3
+    for _ in range(4):
+        eng.step()
+    torch.cuda.synchronize()
+    assert eng.guard_state()["overflows"] == 0
+    assert eng.steps_applied() == 4
+    gmax = eng._gmax.amax(dim=1).cpu()
+    assert float(gmax[1]) > 100 * float(max(gmax[0], gmax[2])), gmax  # really a loud segment between quiet ones
+    _grads(eng, lib)                      # every micro-batch's partials at these weights
+    ga, oa, gga, ka = _grads(eng, lib)    # fused, each at its own scale
+    opts(OPT_HEAD_FUSE, 0)
+    gb, ob, ggb, kb = _grads(eng, lib)    # unfused: the scale from this launch's own max|g|
+    assert ka["head_fwd"] == 3 and kb["head_fwd"] == 0
+    assert torch.equal(oa, ob) and torch.equal(gga, ggb)
+    lay = eng.layout
+    errs = {k: _rel(lay.view(ga, i), lay.view(gb, i)) for i, k in enumerate(lay.names)}
+    for k, e in errs.items():
+        assert e < 2e-5, (k, e)
+    # the round-4 behaviour, for the record: every micro-batch on one max|g| slice
+    opts(OPT_HEAD_FUSE, 1)
+    torch.manual_seed(0)
+    model2 = SirenWithSnakeTanh(1, 1, H, 1, 1, 0, first_omega_0=3000.0, hidden_omega_0=30.0, a_initial=0.5)
+    eng2 = SirenEngine(model2, t, y, micro_batch=mb, device=dev)
+    for b in eng2.batches:
+        b.gmax_part = eng2.batches[0].gmax_part
+    for _ in range(4):
+        eng2.step()
+    torch.cuda.synchronize()
+    shared_overflows = eng2.guard_state()["overflows"]
+    _grads(eng2, lib)
+    gc, _, _, _ = _grads(eng2, lib)
+    opts(OPT_HEAD_FUSE, 0)
+    gd, _, _, _ = _grads(eng2, lib)
+    lay2 = eng2.layout
+    shared_errs = {k: _rel(lay2.view(gc, i), lay2.view(gd, i)) for i, k in enumerate(lay2.names)}
+    log("headfuse_snake_scale_per_micro_batch", errs=errs, gmax=gmax.tolist(), shared_slice_overflows=shared_overflows,
+        shared_slice_errs=shared_errs)

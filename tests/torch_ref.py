@@ -11,16 +11,19 @@ import torch
 
 
 def fp32_fit(state_dict: dict, n_inner: int, omega0: float, coords, target, steps: int, lr: float = 1e-3,
-             patience: int = 200, min_lr: float = 1e-6, omega: float = 30.0, device="cuda"):
+             patience: int = 200, min_lr: float = 1e-6, omega: float = 30.0, device="cuda", factor: float = 0.8,
+             final: bool = False):
     """Sine-only SirenWithSnakeTanh (models.py:114-115, :374-394) fitted full batch; returns
-    (losses [steps], lrs [steps]) as float64 numpy."""
+    (losses [steps], lrs [steps]) as float64 numpy, and with final=True also the model output of
+    the final weights (float32 numpy)."""
     assert not torch.backends.cuda.matmul.allow_tf32
     p = {k: v.detach().clone().float().to(device).requires_grad_(True) for k, v in state_dict.items()}
     names = list(p)
     x = torch.as_tensor(coords, dtype=torch.float32).reshape(-1, p["net.0.linear.weight"].shape[1]).to(device)
     y = torch.as_tensor(target, dtype=torch.float32).reshape(-1, 1).to(device)
     opt = torch.optim.Adam([p[k] for k in names], lr=lr)
-    sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.8, patience=patience, min_lr=min_lr)
+    sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=factor, patience=patience,
+                                                       min_lr=min_lr)
     mse = torch.nn.MSELoss()
 
     def forward():
@@ -39,7 +42,11 @@ def fp32_fit(state_dict: dict, n_inner: int, omega0: float, coords, target, step
         sched.step(loss.detach())
         losses.append(loss.detach())
         lrs.append(sched.get_last_lr()[0])
-    return torch.stack(losses).double().cpu().numpy(), np.array(lrs)
+    out = (torch.stack(losses).double().cpu().numpy(), np.array(lrs))
+    if final:
+        with torch.no_grad():
+            out = out + (forward().reshape(-1).cpu().numpy(),)
+    return out
 
 
 def fp32_fit_stack(state_dict: dict, kinds, omega0: float, coords, target, steps: int, lr: float = 1e-3,

@@ -32,6 +32,11 @@ def main():
     ap.add_argument("--patience", type=int, default=200)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--every", type=int, default=25)
+    ap.add_argument("--omega0", type=float, default=3000.0)
+    ap.add_argument("--factor", type=float, default=0.8)
+    ap.add_argument("--min-lr", type=float, default=1e-6)
+    ap.add_argument("--clip", default="gt_bach_6s.npz", help="tests/golden target file")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 torch comparator")
     args = ap.parse_args()
     import __graft_entry__ as ge
     ge.build()
@@ -40,21 +45,29 @@ def main():
     from inr_for_audio_amd.utils import get_coord
     from torch_ref import fp32_fit
     dev = torch.device("cuda:0")
-    target = np.load(os.path.join(ROOT, "tests", "golden", "gt_bach_6s.npz"))["target"]
+    target = np.load(os.path.join(ROOT, "tests", "golden", args.clip))["target"]
     var = float(np.mean(target.astype(np.float64) ** 2))
     coords = get_coord(target.size, 1).reshape(-1, 1)
     torch.manual_seed(args.seed)
-    m = SirenWithSnakeTanh(1, 1, 1024, 4, 0, 0, first_omega_0=3000.0, hidden_omega_0=30.0)
+    m = SirenWithSnakeTanh(1, 1, 1024, 4, 0, 0, first_omega_0=args.omega0, hidden_omega_0=30.0)
     sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
-    eng = SirenEngine(m, coords, torch.from_numpy(target), lr=args.lr, min_lr=1e-6, patience=args.patience,
-                      hist_cap=args.steps, device=dev)
+    eng = SirenEngine(m, coords, torch.from_numpy(target), lr=args.lr, min_lr=args.min_lr, factor=args.factor,
+                      patience=args.patience, hist_cap=args.steps, device=dev)
     eng.step()
     eng.capture_graph()
     while eng.steps_applied() < args.steps:
         eng.step()
     hip, hip_lr = eng.history()
-    t32, t32_lr = fp32_fit(sd0, 4, 3000.0, coords, target, args.steps, lr=args.lr, patience=args.patience,
-                           device=dev)
+    from inr_for_audio_amd.utils import calculate_snr
+    snr_final_hip = float(calculate_snr(target, eng.infer(coords.to(dev)).cpu().numpy()))
+    if args.no_fp32:
+        t32, t32_lr = hip, hip_lr
+        snr_final_t32 = None
+    else:
+        t32, t32_lr, o32 = fp32_fit(sd0, 4, args.omega0, coords, target, args.steps, lr=args.lr,
+                                    patience=args.patience, device=dev, factor=args.factor, min_lr=args.min_lr,
+                                    final=True)
+        snr_final_t32 = float(calculate_snr(target, o32))
     db = lambda x: 10 * np.log10(var / np.asarray(x))  # noqa: E731
     rows = []
     for k in range(0, args.steps, args.every):
@@ -63,6 +76,9 @@ def main():
                      "lr": float(hip_lr[k])})
         print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
     print(json.dumps({"steps": args.steps, "lr": args.lr, "patience": args.patience, "seed": args.seed,
+                      "omega0": args.omega0, "factor": args.factor, "clip": args.clip,
+                      "snr_target_final_weights_hip": snr_final_hip, "snr_target_final_weights_fp32_gpu": snr_final_t32,
+                      "lr_end": float(hip_lr[-1]),
                       "rows": rows, "final_snr_hip": float(db(hip[-1])), "final_snr_fp32_gpu": float(db(t32[-1])),
                       "overflows": eng.guard_state()["overflows"]}))
 
