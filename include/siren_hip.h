@@ -427,7 +427,8 @@ enum siren_prof_kind {
  * SIREN_OPT_NT_DIAG = measurement-only NT ablations, accepted only by libraries built with
  *   -DSIREN_DIAG (__graft_entry__.build_diagnostic; the product library returns
  *   SIREN_ERR_CONFIG for any non-zero value); results are WRONG while set: bit 0 reads the X
- *   operand from the first 4 row bands only (L2-resident operand); ping-pong K-loop only: bit 2
+ *   operand from the first 4 row bands only (L2-resident operand), bit 3 from the first 256 row bands
+ *   (an X of 128 MB: Infinity-Cache-resident, not L2); ping-pong K-loop only: bit 2
  *   reads W from column tile 0 only (L2-resident W), bit 9 runs no tiles, bit 10 skips the
  *   epilogue (its compute and stores);
  * SIREN_OPT_NT_QUEUE = 1 (default): the ping-pong NT GEMM's persistent blocks take their tiles

@@ -214,19 +214,25 @@ def expected_build_id(defines=()) -> str | None:
     return buildinfo.source_hash(defines) if buildinfo.sources_present() else None
 
 
-def bind(path: str, expect_build_id: str | None = None):
+def bind(path: str, expect_build_id: str | None = None, check_abi: bool = True):
     """A freshly bound (uncached) handle of the library at `path`: tools/ab_bench.py loads the
     product library beside measurement builds of it under other file names.  expect_build_id: refuse
-    a library compiled from other sources (siren_build_id, include/siren_hip.h)."""
+    a library compiled from other sources (siren_build_id, include/siren_hip.h).  check_abi=False
+    (measurement tools only): bind a library of an earlier ABI built from an older commit, for the
+    entry points whose signatures did not change; symbols it lacks are left unbound."""
     if not os.path.exists(path):
         raise SirenError(
             f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (the SIREN path has no eager fallback)")
     lib = ctypes.CDLL(path)
     for name, (res, args) in _SIGS.items():
+        if not check_abi and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if not check_abi:
+        return lib
     if lib.siren_abi_version() != ABI_VERSION:
         raise SirenError(f"libsiren_hip ABI {lib.siren_abi_version()} != expected {ABI_VERSION}")
     if expect_build_id is not None and lib.siren_build_id().decode() != expect_build_id:

@@ -179,8 +179,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   const int G = gridDim.x;
   const int bp = xcd_remap(blockIdx.x, G);
   // measurement-only ablation bits (SIREN_DIAG builds; the queue kernel is launched with none):
-  // 1 X from the first 4 row bands (L2-resident X), 4 W from column tile 0, 512 no tiles,
-  // 1024 no epilogue
+  // 1 X from the first 4 row bands (L2-resident X), 4 W from column tile 0, 8 X from the first 256
+  // row bands (128 MB: beyond L2, inside the Infinity Cache), 512 no tiles, 1024 no epilogue
   const int diag = (SIREN_DIAG_ON && !(Cfg::PP && QUEUE)) ? p.diag : 0;
   const int my_tiles = (diag & 512) ? 0 : (ntiles - bp + G - 1) / G;
   // Dynamic tile queue (ping-pong K-loop, NtParams::tileq).  With the static walk the four
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     m0 = tm * BM;
     n0 = (g - tm * tiles_n) * BN;
   };
-  auto xrow = [&](int m0) { return (diag & 1) ? (m0 & (4 * BM - 1)) : m0; };
+  auto xrow = [&](int m0) { return (diag & 1) ? (m0 & (4 * BM - 1)) : (diag & 8) ? (m0 & (256 * BM - 1)) : m0; };
 
   // ---- LDS-DMA staging addresses (non-ping-pong K-loops) ------------------------------
   // One instruction moves 1 KiB = RPI rows x ROWB bytes.  Lane L lands at row L/SPR, 16-B

@@ -69,11 +69,11 @@ def fwd_bwd(model, coords, target):
     return out.detach().numpy().reshape(-1), float(loss), grads
 
 
-def restated_loop(model, coords, target, steps, lr=1e-3, min_lr=1e-6, patience=200):
+def restated_loop(model, coords, target, steps, lr=1e-3, min_lr=1e-6, patience=200, factor=0.8):
     """run.py:156-187 on CPU around the reference model (alpha=0: the STFT term is exactly
     zero; best_model aliases model, run.py:173)."""
     opt = torch.optim.Adam(model.parameters(), lr=lr)
-    sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.8, patience=patience,
+    sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=factor, patience=patience,
                                                        min_lr=min_lr)
     mse = torch.nn.MSELoss()
     x = coords.reshape(1, coords.shape[0], -1)
@@ -320,7 +320,7 @@ def checkpoint_fixture(ref_models, ref_utils):
 
 
 def fullsize_seed_trajectories(ref_models, ref_utils, seeds, steps, patience, omega0=3000.0, lr=1e-3,
-                               fname="trajectory_5x1024_w3000_seeds.json", duration=1):
+                               fname="trajectory_5x1024_w3000_seeds.json", duration=1, factor=0.8, min_lr=1e-6):
     """The headline model (SIREN 5x1024, BASELINE cfg2's shape) fitted full batch on gt_bach
     (`duration` s: 1, or 6 = 264 600 coordinates, the longest whole-second clip gt_bach holds
     and the closest to cfg2's 10 s) over several init seeds -- the 0.1 dB fit-parity fixture at
@@ -332,17 +332,19 @@ def fullsize_seed_trajectories(ref_models, ref_utils, seeds, steps, patience, om
     tgt = target.numpy().reshape(-1)
     path = os.path.join(OUT, fname)
     out = {"steps": steps, "omega0": omega0, "hidden": 1024, "num_sine": 4, "patience": patience,
-           "factor": 0.8, "lr0": lr, "duration": duration, "runs": {}}
+           "factor": factor, "lr0": lr, "min_lr": min_lr, "duration": duration, "runs": {}}
     if os.path.exists(path):
         prev = json.load(open(path))
-        if all(prev.get(k, 1 if k == "duration" else None) == out[k]
-               for k in ("steps", "omega0", "patience", "lr0", "duration")):
+        if all(prev.get(k, {"duration": 1, "factor": 0.8, "min_lr": 1e-6}.get(k)) == out[k]
+               for k in ("steps", "omega0", "patience", "lr0", "duration", "factor", "min_lr")):
             out["runs"] = prev["runs"]
+            out.update({k: v for k, v in prev.items() if k not in out})  # e.g. fp32_gpu (tools/fit6_probe.py)
     for s in seeds:
         if str(s) in out["runs"]:
             continue
         m = siren(ref_models, 1024, 4, omega0, seed=s)
-        losses, lrs, final = restated_loop(m, coords, target, steps, lr=lr, patience=patience)
+        losses, lrs, final = restated_loop(m, coords, target, steps, lr=lr, patience=patience, min_lr=min_lr,
+                                           factor=factor)
         out["runs"][str(s)] = {"loss": losses.tolist(), "lr": lrs.tolist(),
                                "snr_target": float(ref_utils.calculate_snr(tgt, final))}
         print(f"5x1024 seed {s}: final {losses[-1]:.3e} min {losses.min():.3e} lr_end {lrs[-1]:.3e} "
@@ -358,6 +360,9 @@ def main():
     ap.add_argument("--lr", type=float, default=1e-3, help="--fullsize-seeds: Adam lr")
     ap.add_argument("--fullsize-file", default="trajectory_5x1024_w3000_seeds.json")
     ap.add_argument("--duration", type=int, default=1, help="--fullsize-seeds: seconds of gt_bach")
+    ap.add_argument("--omega0", type=float, default=3000.0, help="--fullsize-seeds: first-layer omega_0")
+    ap.add_argument("--factor", type=float, default=0.8, help="--fullsize-seeds: ReduceLROnPlateau factor")
+    ap.add_argument("--min-lr", type=float, default=1e-6, help="--fullsize-seeds: ReduceLROnPlateau min_lr")
     ap.add_argument("--clip", type=int, default=0, help="write only gt_bach_<clip>s.npz: the WaveformFitting "
                     "target of the first <clip> seconds (the data of the --duration fixtures)")
     ap.add_argument("--seeds", default="0,1,2,3,4", help="init seeds of the multi-seed trajectories")
@@ -395,7 +400,8 @@ def main():
     if args.fullsize_seeds:
         fullsize_seed_trajectories(ref_models, ref_utils, [int(s) for s in args.fullsize_seeds.split(",")],
                                    args.trajectory_steps, args.patience, lr=args.lr, fname=args.fullsize_file,
-                                   duration=args.duration)
+                                   duration=args.duration, omega0=args.omega0, factor=args.factor,
+                                   min_lr=args.min_lr)
         return
     if args.only_seeds:
         seed_trajectories(ref_models, ref_utils, [int(s) for s in args.seeds.split(",")],

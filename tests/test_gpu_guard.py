@@ -67,7 +67,7 @@ def test_no_overflow_leaves_scale_alone(dev):
     eng, _, _, _ = _setup(dev, 1.0)
     eng.run(5)
     gs = eng.guard_state()
-    assert gs == {"headroom": 6, "overflows": 0, "clean": 5}
+    assert gs == {"headroom": 6, "overflows": 0, "clean": 5, "stalls": 0}
     assert eng.steps_applied() == 5
 
 
