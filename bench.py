@@ -229,7 +229,7 @@ def dp_report(eng, args, dev, dist, steps: int = 5) -> dict:
 
 # recon SNR fixtures (the metric's second half), newest first: the reference's own fit of the
 # headline model on gt_bach, written by tests/golden/make_golden.py in the build container
-RECON_FIXTURES = [("fit_5x1024_6s_converged.json", "gt_bach_6s.npz"),
+RECON_FIXTURES = [("fit_5x1024_w18000_6s.json", "gt_bach_6s.npz"),
                   ("trajectory_5x1024_w3000_lr3e-5_seeds.json", "gt_bach_1s.npz")]
 
 
