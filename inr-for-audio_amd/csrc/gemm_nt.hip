@@ -45,19 +45,6 @@
 #define SIREN_SNAKE0_EB 2
 #endif
 
-// forward modes, ping-pong K-loop: at the start of a tile's epilogue, prefetch the next tile's X rows
-// (K-tiles 2.., this column block's share of the band) into L2 / the Infinity Cache
-#ifndef SIREN_NT_PF
-#define SIREN_NT_PF 0
-#endif
-
-// ping-pong K-loop: column tile c of a row band walks its K-tiles from (c * SIREN_NT_KROT) mod nk, so
-// the band's column blocks do not all miss L2 on the same X lines at the same time (the first to
-// reach a K-tile fetches it, the others find it in L2); 0 = every tile from K-tile 0
-#ifndef SIREN_NT_KROT
-#define SIREN_NT_KROT 0
-#endif
-
 #ifdef SIREN_DIAG
 #define SIREN_DIAG_ON 1
 #else
@@ -113,8 +100,7 @@ struct NtLds {
   static constexpr int A = HW + (HEAD ? Cfg::VEC : 0);
   static constexpr int IA = A + (nt_is_snake_fwd(MODE) ? Cfg::VEC : 0);   // Snake 1/a, divided once
   static constexpr int QS = IA + (nt_is_snake_fwd(MODE) ? Cfg::VEC : 0);  // dynamic tile queue: 2 tile ids
-  static constexpr int PF = QS + 16;  // prefetch landing words (256 B; never read)
-  static constexpr int SIZE = PF + 256;
+  static constexpr int SIZE = QS + 16;
   static_assert(SIZE <= 160 * 1024, "LDS");
 };
 
@@ -914,7 +900,6 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     // operand bases of the current tile (0) and the next one (1), set once per tile:
     // no division or 64-bit product in the per-phase scalar work
     const h16 *x0 = p.X, *x1 = p.X, *w0 = p.W, *w1 = p.W;
-    int kr0 = 0, kr1 = 0;  // K-tile rotation of the current / next tile (SIREN_NT_KROT)
     // This block's current and next tile (global ids); the next one exists while it lies in
     // [g_lo, g_lim).  Static walk: bp, bp + G, ...  Queue: shard s = blockIdx % 8 (one XCD under
     // round-robin dispatch -- speed only, any placement is correct) pulls tiles
@@ -946,24 +931,18 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         // queue: the pull tile_end(ti - 1) left in the slot
         g_next = dyn ? __builtin_amdgcn_readfirstlane(qslot[0]) : g_next + G;
       }
-      auto bases = [&](int g, const h16*& xb, const h16*& wb, int& kr) {
+      auto bases = [&](int g, const h16*& xb, const h16*& wb) {
         int m0, n0;
         tile_of(g, m0, n0);
         xb = p.X + (size_t)xrow(m0) * K;
         wb = p.W + (size_t)((diag & 4) ? 0 : n0) * K;  // diag bit 2: one W column tile (L2-resident W)
-        kr = SIREN_NT_KROT ? ((n0 / BN) * SIREN_NT_KROT) % nk : 0;
       };
-      bases(g_cur, x0, w0, kr0);
-      bases(in_range(g_next) ? g_next : g_cur, x1, w1, kr1);
+      bases(g_cur, x0, w0);
+      bases(in_range(g_next) ? g_next : g_cur, x1, w1);
     };
     auto issue = [&](int sel, int kt, int slot, auto pcc) {
       constexpr int PC = decltype(pcc)::value;
-      int kp = kt;
-      if constexpr (SIREN_NT_KROT != 0) {
-        kp += sel ? kr1 : kr0;
-        kp -= kp >= nk ? nk : 0;
-      }
-      const h16* src = ((PC & 1) ? (sel ? x1 : x0) : (sel ? w1 : w0)) + kp * BK;
+      const h16* src = ((PC & 1) ? (sel ? x1 : x0) : (sel ? w1 : w0)) + kt * BK;
       const char* dst = smem + slot * Cfg::STAGE;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -1008,23 +987,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             __builtin_amdgcn_mfma_f32_16x16x32_f16(a, xf[jl][kk], acc[2 * NH + il][4 * MH + jl], 0, 0, 0);
       }
     };
-    // the next tile's X rows for K-tiles 2..nk-1 (its K-tiles 0, 1 are already in flight): the
-    // tiles_n blocks of a band each take 1/tiles_n of its rows, one 128-B line per lane per K-tile
-    auto prefetch_next = [&]() {
-      if (!in_range(g_next)) return;
-      int m0n, n0n;
-      tile_of(g_next, m0n, n0n);
-      const int rp = BM / tiles_n, ngrp = (rp + 63) / 64;
-      const int nins = ngrp * (nk - 2);
-      const char* base = (const char*)x1 + (size_t)(n0n / BN) * rp * K * 2;
-      for (int i = wave; i < nins; i += Cfg::NWAVES) {
-        const int kt = 2 + i / ngrp, r = (i % ngrp) * 64 + lane;
-        if (r < rp) gpf4_asm(base + ((size_t)r * K + kt * BK) * 2, lds_addr(smem + Lay::PF));
-      }
-    };
     auto tile_end = [&](int) {
       // both groups are aligned here
-      if constexpr (SIREN_NT_PF && nt_is_fwd(MODE) && !nt_is_snake_fwd(MODE)) prefetch_next();
       pre(g_cur);
       int pend = 0;  // the tile after next
       if (dyn && wave == 0)
@@ -1041,7 +1005,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
     pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles,
-                                                         tile_end, more);
+                                                       tile_end, more);
   } else {
     mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
         my_tiles, K / BK, acc, stage, frags, [&](int ti) { pre(bp + ti * G); },

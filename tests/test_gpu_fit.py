@@ -204,19 +204,19 @@ def test_fit_headline_model_stable_regime_per_seed(dev):
         assert v["max_step_db"] < 0.1, (s, v)
 
 
-def _fit6(dev, steps, seed, patience, lr):
-    """SIREN 5x1024, omega0 3000, on gt_bach 6 s (264 600 coordinates: a quarter of cfg2's 2^20
-    rows, the longest whole-second clip of the reference's gt_bach.wav): the fused path with
-    its production settings (256 tiles, fused head backward, graph replay)."""
+def _fit6(dev, steps, seed, patience, lr, omega0=3000.0, factor=0.8, min_lr=1e-6):
+    """SIREN 5x1024 on gt_bach 6 s (264 600 coordinates: a quarter of cfg2's 2^20 rows, the
+    longest whole-second clip of the reference's gt_bach.wav): the fused path with its production
+    settings (256 tiles, fused head backward, graph replay)."""
     from inr_for_audio_amd.engine import SirenEngine
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     from inr_for_audio_amd.utils import calculate_snr, get_coord
     target = np.load(os.path.join(G, "gt_bach_6s.npz"))["target"]
     coords = get_coord(target.size, 1).reshape(-1, 1)
     torch.manual_seed(seed)
-    m = SirenWithSnakeTanh(1, 1, 1024, 4, 0, 0, first_omega_0=3000.0, hidden_omega_0=30.0)
-    eng = SirenEngine(m, coords, torch.from_numpy(target), lr=lr, min_lr=1e-6, patience=patience, hist_cap=steps,
-                      device=dev)
+    m = SirenWithSnakeTanh(1, 1, 1024, 4, 0, 0, first_omega_0=omega0, hidden_omega_0=30.0)
+    eng = SirenEngine(m, coords, torch.from_numpy(target), lr=lr, min_lr=min_lr, factor=factor, patience=patience,
+                      hist_cap=steps, device=dev)
     assert eng.lib.siren_nt_tile(eng.rows, 1024) == 256
     eng.step()
     eng.capture_graph()
@@ -269,17 +269,68 @@ STEP_DB = 0.01
 STABLE_STEPS_6S = 80
 
 
+# the fixed-gate reconstruction fixture: omega0 18000 (the 1 s fixtures' 3000 per
+# second of audio), lr 1e-5, 140 full-batch steps -- SNR_target 22.3 dB in the regime where the
+# reference's trajectory does not depend on summation order.  Probed on the GPU (tools/fit6_probe.py,
+# profiles/r17/probe6s_*.json): every run at omega0 9000-24000 and lr 1e-5 .. 1e-4 keeps two
+# implementations within 0.01-0.03 dB until Adam's first loss spike (step 130-210 here), after which
+# they land 0.1-1 dB apart even when ReduceLROnPlateau anneals (patience 3, factor 0.5: 0.083 dB at
+# step 300); 140 steps stay before that spike on every run probed at this setting
+FIXED_6S = "fit_5x1024_w18000_6s.json"
+STEP_DB_18K = 0.05   # per-step loss gate of that run (fp32 torch on the GPU: <= 0.011 dB by step 150)
+
+
+def test_fit_headline_model_6s_fixed_snr_gate(dev):
+    """North_star's "reconstruction SNR within 0.1 dB of the reference" at a FIXED 0.1 dB: SIREN 5x1024
+    on gt_bach 6 s, fitted to SNR_target > 20 dB against the reference's own runs (make_golden.py
+    --fullsize-seeds 0,1 --duration 6 --omega0 18000 --lr 1e-5 --trajectory-steps 140).  Per seed:
+    SNR_target of the final weights (utils.py:77-97, what run.py:302-335 reports) within 0.1 dB of the
+    reference's, every step's loss within STEP_DB_18K, the lr trace identical; and plain fp32 torch on
+    the GPU (the reference algorithm with only its summation order changed) lands within 0.05 dB of the
+    reference at the last step -- the fixture's own acceptance check."""
+    from torch_ref import fp32_fit
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    from inr_for_audio_amd.utils import calculate_snr, get_coord
+    ref = json.load(open(os.path.join(G, FIXED_6S)))
+    assert ref["duration"] == 6 and ref["hidden"] == 1024 and ref["omega0"] == 18000.0
+    target = np.load(os.path.join(G, "gt_bach_6s.npz"))["target"]
+    coords = get_coord(target.size, 1).reshape(-1, 1)
+    rows = {}
+    for s in sorted(int(k) for k in ref["runs"]):
+        r = ref["runs"][str(s)]
+        assert r["snr_target"] > 20.0, r["snr_target"]
+        eng, snr, var = _fit6(dev, ref["steps"], s, ref["patience"], ref["lr0"], omega0=ref["omega0"],
+                              factor=ref["factor"], min_lr=ref["min_lr"])
+        losses, lrs = eng.history()
+        rl = np.array(r["loss"])
+        torch.manual_seed(s)
+        sd = SirenWithSnakeTanh(1, 1, 1024, 4, 0, 0, first_omega_0=ref["omega0"], hidden_omega_0=30.0).state_dict()
+        t32, _, o32 = fp32_fit(sd, 4, ref["omega0"], coords, target, ref["steps"], lr=ref["lr0"],
+                               patience=ref["patience"], factor=ref["factor"], min_lr=ref["min_lr"], device=dev,
+                               final=True)
+        rows[s] = {"snr_target_gpu": snr, "snr_target_ref": r["snr_target"],
+                   "snr_target_torch_gpu_fp32": float(calculate_snr(target, o32)),
+                   "max_step_db": float(np.max(np.abs(10 * np.log10(losses / rl)))),
+                   "max_step_db_torch_gpu_fp32": float(np.max(np.abs(10 * np.log10(t32 / rl))))}
+        assert np.array_equal(lrs, np.array(r["lr"])), s
+    log("fit_5x1024_6s_fixed_gate", seeds=rows)
+    print("\n" + json.dumps(rows, indent=1))
+    for s, v in rows.items():
+        assert abs(v["snr_target_gpu"] - v["snr_target_ref"]) < 0.1, (s, v)
+        assert v["max_step_db"] < STEP_DB_18K, (s, v)
+        assert abs(v["snr_target_torch_gpu_fp32"] - v["snr_target_ref"]) < 0.05, (s, v)
+
+
 def test_fit_headline_model_6s_converged(dev):
-    """cfg2's model on cfg2-scale data fitted to the reference's converged
+    """cfg2's model on cfg2-scale data fitted towards the reference's converged
     reconstruction -- SIREN 5x1024, omega0 3000, gt_bach 6 s (264 600 coordinates), 400 full-batch
     steps at lr 3e-5, seed 0, against the reference's own run (make_golden.py --fullsize-seeds 0
     --duration 6 --trajectory-steps 400: SNR_target 14.53 dB, best-loss SNR 14.79 dB; the SNR still
     rises ~0.2 dB per 25 steps there, so 20 dB is several thousand CPU steps away).  Gates: every
-    step of the stable window within STEP_DB; the best-loss SNR within north_star's 0.1 dB; the final
-    reconstruction SNR (SNR_target of the final weights, utils.py:77-97) within 0.1 dB plus how far
-    the reference algorithm itself lands from the CPU run when only its summation order changes
-    (fp32 torch on this GPU, same init and data), since past step ~100 the fit is in the regime
-    where Adam's loss oscillations amplify rounding (test_fit_quality_headline_model_over_seeds)."""
+    step of the stable window within STEP_DB and the best-loss SNR within north_star's 0.1 dB.  The
+    final reconstruction SNR is logged only: past step ~100 this fit is in the regime where Adam's loss
+    oscillations amplify rounding (fp32 torch on the GPU ends 0.36 dB from the CPU run), so it cannot
+    carry a fixed 0.1 dB gate; test_fit_headline_model_6s_fixed_snr_gate does."""
     from torch_ref import fp32_fit
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     from inr_for_audio_amd.utils import get_coord
@@ -307,6 +358,6 @@ def test_fit_headline_model_6s_converged(dev):
     assert np.array_equal(lrs, np.array(r["lr"]))
     assert row["max_step_db_stable"] < STEP_DB, row
     assert abs(row["best_gpu"] - row["best_ref"]) < 0.1, row
-    # final reconstruction SNR; the yardstick is the fp32 torch run's distance from the CPU run at the
-    # last step (loss-based: the fp32 path's final weights are not kept)
-    assert abs(row["final_snr_gpu"] - row["final_snr_ref"]) < 0.1 + abs(row["last_torch_gpu_fp32"] - row["last_ref"]), row
+    # the final weights of this run come out of Adam's oscillating regime, where the reference itself
+    # is not reproducible to 0.1 dB (fp32 torch on the GPU ends 0.36 dB from it): logged, not gated
+    # here -- the fixed 0.1 dB reconstruction gate is test_fit_headline_model_6s_fixed_snr_gate's

@@ -28,6 +28,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="fwd,fwd_head,fwd_hb,dx,dx0,dw", help="cases")
+    ap.add_argument("--grid", type=int, default=0, help="SIREN_OPT_NT_GRID for every library (0: one block per CU)")
+    ap.add_argument("--queue", type=int, default=1, help="SIREN_OPT_NT_QUEUE for every library")
+    ap.add_argument("--own-out", action="store_true", help="time every library on its own output buffers "
+                    "(default: all on the first library's, since buffer placement alone moved a forward "
+                    "by ~2 %% between identical kernels, profiles/r17)")
     args = ap.parse_args()
     from inr_for_audio_amd import _lib
     libs = {}
@@ -35,6 +40,8 @@ def main():
         nm, path = item.split("=")
         # libraries built from older commits (tools/build_at.py) may carry an earlier ABI
         libs[nm] = _lib.bind(os.path.join(ROOT, path), check_abi=False)
+    for lib_ in libs.values():
+        assert lib_.siren_set_option(4, args.grid) == 0 and lib_.siren_set_option(8, args.queue) == 0
     dev = torch.device("cuda:0")
     R, H = args.rows, args.hidden
     s = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
@@ -68,8 +75,8 @@ def main():
     slab = torch.empty(int(list(libs.values())[0].siren_slab_floats(H, splits)), device=dev)
     flops = 2.0 * R * H * H
 
-    def case(nm, lib, kind):
-        o = outs[nm]
+    def case(nm, lib, kind, onm=None):
+        o = outs[onm or nm]
         if kind == "fwd":
             return lambda: lib.siren_inner_fwd(P(X), P(W), P(b), ctypes.c_float(30.0), R, H, P(o["Y"]), P(o["C"]),
                                                None, None, P(tq), s())
@@ -127,9 +134,16 @@ def main():
                     mism[f"{tag}:{nm}:{k}"] = [bool(torch.equal(a, c)) for a, c in zip(got[nm], got[base])]
 
     parity("pre")
+    if not args.own_out:  # timing on one set of output buffers
+        first = next(iter(libs))
+        cases = {(nm, k): case(nm, lib, k, first) for k in kinds for nm, lib in libs.items()}
     times = {key: [] for key in cases}
-    for _ in range(args.rounds):
-        for key, fn in cases.items():
+    names = list(libs)
+    for rnd in range(args.rounds):
+        # the library order rotates every round: the first case of a round runs measurably slower
+        # (profiles/r17: 3-4 % in u4's two orders), so no library may always take that place
+        order = names[rnd % len(names):] + names[:rnd % len(names)]
+        for key, fn in sorted(cases.items(), key=lambda kv: (kinds.index(kv[0][1]), order.index(kv[0][0]))):
             fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -138,6 +152,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[key].append(e0.elapsed_time(e1) / args.reps)
+    cases = {(nm, k): case(nm, lib, k) for k in kinds for nm, lib in libs.items()}
     parity("post")
     res = {}
     for (nm, k), ts in times.items():

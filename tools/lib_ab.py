@@ -21,7 +21,7 @@ from inr_for_audio_amd import _lib
 lib = _lib.load({lib!r})
 for opt, val in {opts!r}:
     _lib.check(lib.siren_set_option(opt, val), "set_option")
-sys.argv = ["bench.py", "--config", {cfg!r}, "--steps", "10", "--warmup", "3", "--no-cpu-baseline"]
+sys.argv = ["bench.py", "--config", {cfg!r}, "--steps", "10", "--warmup", "3", "--no-cpu-baseline", "--no-recon-snr"]
 runpy.run_path({bench!r}, run_name="__main__")
 """
 
