@@ -14,7 +14,7 @@ import os
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 HEADER = os.path.join(os.path.dirname(PKG), "include", "siren_hip.h")
-SOURCES = ["capi.hip", "gemm_nt.hip", "gemm_tn.hip", "elementwise.hip", "kan.hip", "layer_fp32.hip"]
+SOURCES = ["capi.hip", "gemm_nt.hip", "gemm_nt1.hip", "gemm_nt2.hip", "gemm_tn.hip", "elementwise.hip", "kan.hip", "layer_fp32.hip"]
 HEADERS = ["siren_common.h", "siren_kernels.h", "gemm_pipeline.h"]
 ARCH = "gfx950"
 FLAGS = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",

@@ -734,7 +734,7 @@ int siren_set_option(int32_t option, int32_t value) {
       else gemm_tn_set_tile(value);
       return SIREN_OK;
     case SIREN_OPT_NT_PIPE:
-      if (value != -1 && value != 0 && value != 1 && value != 4) return SIREN_ERR_CONFIG;
+      if (value != -1 && value != 0 && value != 1 && (value < 4 || value > 7)) return SIREN_ERR_CONFIG;
       gemm_nt_set_pipe(value);
       return SIREN_OK;
     case SIREN_OPT_TN_PIPE:
@@ -746,7 +746,7 @@ int siren_set_option(int32_t option, int32_t value) {
       gemm_nt_set_grid_cap(value);
       return SIREN_OK;
     case SIREN_OPT_NT_DIAG:
-      if (value < 0 || (value & ~(1 | 4 | 8 | 512 | 1024))) return SIREN_ERR_CONFIG;
+      if (value < 0 || (value & ~(1 | 4 | 8 | 512 | 1024 | 2048))) return SIREN_ERR_CONFIG;
       return gemm_nt_set_diag(value) ? SIREN_OK : SIREN_ERR_CONFIG;
     case SIREN_OPT_NT_QUEUE:
       if (value < 0 || value > 2) return SIREN_ERR_CONFIG;

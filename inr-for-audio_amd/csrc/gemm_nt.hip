@@ -1154,7 +1154,7 @@ static hipError_t dispatch_act(int mode, bool head, const NtParams& p, hipStream
 // tile per block; 1 = BK 64 persistent; 4 = BK 64 persistent ping-pong (pingpong_tiles)
 static int g_nt_tile = 0;
 static int g_nt_pipe = -1;  // -1: automatic = ping-pong 4 for every mode (kernel_bench r06)
-static bool nt_pp() { return g_nt_pipe < 0 || g_nt_pipe == 4; }
+static bool nt_pp() { return g_nt_pipe < 0 || (g_nt_pipe >= 4 && g_nt_pipe <= 7); }
 void gemm_nt_set_tile(int tile) { g_nt_tile = tile; }
 void gemm_nt_set_pipe(int v) { g_nt_pipe = v; }
 
@@ -1208,9 +1208,18 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (p.tile == 256) {
     if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
     const int pipe = g_nt_pipe >= 0 ? g_nt_pipe : 4;
+    // pipe 5: the forward with its epilogue under the next tile's MFMAs (gemm_nt1.hip)
+    if ((pipe == 5 || pipe == 7) && mode == NT_FWD && !head && gemm_nt_one_ok(p))
+      return gemm_nt_one(p, g_nt_grid_cap > 0 ? g_nt_grid_cap : stream_cus(s), g_nt_diag, pipe == 5, s);
+    // pipe 6: the forward with one wave per SIMD on 256x256 tiles (gemm_nt2.hip)
+    if (pipe == 6 && mode == NT_FWD && !head && gemm_nt_big_ok(p))
+      return gemm_nt_big(p, g_nt_grid_cap > 0 ? g_nt_grid_cap : stream_cus(s), g_nt_diag, s);
     switch (pipe) {
       case 0: return dispatch_mode<NtLarge>(mode, head, p, s, false);
-      case 4: return dispatch_mode<NtLargePP>(mode, head, p, s, true);
+      case 4:
+      case 5:  // (pipes 5-7 cover the plain forward only; every other mode takes the ping-pong)
+      case 6:
+      case 7: return dispatch_mode<NtLargePP>(mode, head, p, s, true);
       default: return dispatch_mode<NtLarge>(mode, head, p, s, true);
     }
   }

@@ -74,6 +74,14 @@ constexpr int kTileqInts = 768;  // == SIREN_TILEQ_INTS (include/siren_hip.h)
 
 int nt_choose_tile(int M, int N);
 hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s);
+// the forward (NT_FWD, no head) with its epilogue under the next tile's MFMAs: one wave per SIMD,
+// 128x256 tiles, K / 64 in {4, 8, 16}, N / 256 in {1, 2, 4} (gemm_nt1.hip; SIREN_OPT_NT_PIPE 5)
+bool gemm_nt_one_ok(const NtParams& p);
+hipError_t gemm_nt_one(const NtParams& p, int grid, int diag, bool overlap, hipStream_t s);  // pipe 5 / 7
+// the forward (NT_FWD, no head) with one wave per SIMD on 256x256 tiles, BK 32, 4-stage ring:
+// K % 128 == 0, N / 256 in {1, 2, 4} (gemm_nt2.hip; SIREN_OPT_NT_PIPE 6)
+bool gemm_nt_big_ok(const NtParams& p);
+hipError_t gemm_nt_big(const NtParams& p, int grid, int diag, hipStream_t s);
 // NT_FWD_HB is available for this shape under the current tile / K-loop settings
 // also false when the fused launch's grid could not be co-resident (occupancy x CUs < grid)
 bool gemm_nt_head_fusable(int M, int N, hipStream_t s, int mode = NT_FWD_HB);

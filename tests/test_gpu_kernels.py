@@ -52,7 +52,8 @@ def _release():
 
 
 @pytest.fixture(params=[(128, 0, 0), (256, 0, 0), (256, 1, 0), (256, 1, 2), (256, 1, 3), (256, 4, 0),
-                        (256, 4, 2), (256, 4, 3), (256, 4, 5)],
+                        (256, 4, 2), (256, 4, 3), (256, 4, 5), (256, 5, 0), (256, 5, 3), (256, 6, 0),
+                        (256, 6, 3), (256, 7, 0), (256, 7, 3)],
                 ids=lambda p: f"t{p[0]}p{p[1]}g{p[2]}")
 def nt_tile(request, lib):
     """Force the NT GEMM tile edge, persistence and persistent grid size (siren_set_option)
@@ -160,6 +161,41 @@ def test_inner_fwd(lib, dev, R, H, head, nt_tile):
         ref = np.sin(a) @ hw.astype(np.float64)
         got = hp.cpu().numpy().astype(np.float64).sum(0)
         assert np.max(np.abs(got - ref)) < 1e-4 * max(1.0, np.max(np.abs(ref)))
+
+
+@pytest.mark.parametrize("R,H,grid", [(512, 256, 0), (4096, 512, 7), (65536, 1024, 0), (220160, 512, 0),
+                                      (262144, 1024, 37)])
+def test_inner_fwd_pipes_bit_identical(lib, dev, R, H, grid):
+    """The one-wave-per-SIMD forwards (SIREN_OPT_NT_PIPE 5: 128x256 tiles with the epilogue under the
+    next tile's MFMAs, gemm_nt1.hip; 7: the same K loop with the epilogue at the tile's end; 6: 256x256
+    tiles, BK 32, 4-stage ring, gemm_nt2.hip) against the
+    ping-pong forward (pipe 4): Y and C bit-identical (same K order per output, same epilogue
+    arithmetic), every block walking 1 .. 100+ tiles."""
+    g = torch.Generator(device=dev).manual_seed(R + H)
+    X = torch.sin(torch.rand(R, H, device=dev, generator=g) * 6.2831853).to(H16)
+    lim = math.sqrt(6 / H) / 30
+    W = ((torch.rand(H, H, device=dev, generator=g) * 2 - 1) * lim).to(H16)
+    b = (torch.rand(H, device=dev, generator=g) - 0.5) * 0.06
+    tq = new_tileq(dev)
+    outs = {}
+    try:
+        ok(lib.siren_set_option(0, 256), lib)
+        ok(lib.siren_set_option(4, grid), lib)
+        for pipe in (4, 5, 6, 7):
+            ok(lib.siren_set_option(2, pipe), lib)
+            Y = torch.full((R, H), float("nan"), dtype=H16, device=dev)
+            C = torch.full_like(Y, float("nan"))
+            ok(lib.siren_inner_fwd(ptr(X), ptr(W), ptr(b), ctypes.c_float(30.0), R, H, ptr(Y), ptr(C), None,
+                                   None, ptr(tq), S()), lib)
+            torch.cuda.synchronize()
+            outs[pipe] = (Y.view(torch.int16), C.view(torch.int16))
+    finally:
+        lib.siren_set_option(0, 0)
+        lib.siren_set_option(2, -1)
+        lib.siren_set_option(4, 0)
+    for pipe in (5, 6, 7):
+        assert torch.equal(outs[pipe][0], outs[4][0]), pipe
+        assert torch.equal(outs[pipe][1], outs[4][1]), pipe
 
 
 def test_head_loss(lib, dev):

@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 
 # (rows, hidden, grid cap): tiles per block 1, 2, 3, odd / even, every K / N variant
 PARITY = [(256, 256, 0), (512, 512, 0), (256, 1024, 3), (1024, 1024, 5), (2048, 512, 7), (4096, 1024, 8),
-          (65536, 1024, 0), (220160, 512, 0), (1 << 20, 1024, 0), (1 << 20, 1024, 37)]
+          (4096, 256, 0), (65536, 1024, 0), (220160, 512, 0), (1 << 20, 1024, 0), (1 << 20, 1024, 37)]
 
 
 def main():
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--skip-parity", action="store_true")
+    ap.add_argument("--pipes", default="5,6", help="NT pipes checked against the ping-pong forward (pipe 4)")
     args = ap.parse_args()
     from inr_for_audio_amd import _lib
     lib = _lib.load()
@@ -48,6 +49,7 @@ def main():
         R, H = X.shape
         _lib.check(lib.siren_set_option(2, pipe), "pipe")
         _lib.check(lib.siren_set_option(4, grid), "grid")
+        _lib.check(lib.siren_set_option(0, 256), "tile")
         return lib.siren_inner_fwd(X.data_ptr(), W.data_ptr(), b.data_ptr(), ctypes.c_float(30.0), R, H,
                                    Y.data_ptr(), C.data_ptr(), None, None, tq.data_ptr(), s())
 
@@ -56,22 +58,26 @@ def main():
         for R, H, grid in PARITY:
             X, W, b = make(R, H, seed=R + H)
             ys = []
-            for pipe in (4, 5):
+            pipes = [4] + [int(x) for x in args.pipes.split(",")]
+            for pipe in pipes:
                 Y = torch.full((R, H), float("nan"), dtype=f16, device=dev)
                 C = torch.full((R, H), float("nan"), dtype=f16, device=dev)
                 _lib.check(fwd(pipe, grid, X, W, b, Y, C), f"fwd pipe {pipe}")
                 torch.cuda.synchronize()
                 ys.append((Y, C))
-            same = bool(torch.equal(ys[0][0].view(torch.int16), ys[1][0].view(torch.int16)) and
-                        torch.equal(ys[0][1].view(torch.int16), ys[1][1].view(torch.int16)))
-            nan = bool(torch.isnan(ys[1][0]).any() or torch.isnan(ys[1][1]).any())
-            row = {"rows": R, "hidden": H, "grid": grid, "bit_identical": same, "nan_left": nan}
-            if not same:
-                d = (ys[0][0].float() - ys[1][0].float()).abs()
-                row["max_abs_Y"] = float(torch.nan_to_num(d, nan=99.0).max())
-                bad = torch.nonzero(torch.nan_to_num(d, nan=99.0) > 0)
-                row["first_bad"] = bad[:4].tolist()
-                row["n_bad"] = int(bad.shape[0])
+            row = {"rows": R, "hidden": H, "grid": grid}
+            for q in range(1, len(pipes)):
+                same = bool(torch.equal(ys[0][0].view(torch.int16), ys[q][0].view(torch.int16)) and
+                            torch.equal(ys[0][1].view(torch.int16), ys[q][1].view(torch.int16)))
+                nan = bool(torch.isnan(ys[q][0]).any() or torch.isnan(ys[q][1]).any())
+                r = {"bit_identical": same, "nan_left": nan}
+                if not same:
+                    d = (ys[0][0].float() - ys[q][0].float()).abs()
+                    r["max_abs_Y"] = float(torch.nan_to_num(d, nan=99.0).max())
+                    bad = torch.nonzero(torch.nan_to_num(d, nan=99.0) > 0)
+                    r["first_bad"] = bad[:4].tolist()
+                    r["n_bad"] = int(bad.shape[0])
+                row[f"pipe{pipes[q]}"] = r
             out["parity"].append(row)
             print(json.dumps(row), flush=True)
             del X, W, b, ys
@@ -81,9 +87,10 @@ def main():
         X, W, b = make(R, H)
         Y = torch.empty(R, H, dtype=f16, device=dev)
         C = torch.empty_like(Y)
-        times = {4: [], 5: []}
+        pl = [4] + [int(x) for x in args.pipes.split(",")]
+        times = {q: [] for q in pl}
         for rnd in range(args.rounds):
-            for pipe in ((4, 5) if rnd % 2 == 0 else (5, 4)):
+            for pipe in pl[rnd % len(pl):] + pl[:rnd % len(pl)]:
                 _lib.check(fwd(pipe, 0, X, W, b, Y, C), "warm")
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -105,6 +112,7 @@ def main():
         torch.cuda.empty_cache()
     lib.siren_set_option(2, -1)
     lib.siren_set_option(4, 0)
+    lib.siren_set_option(0, 0)
     print(json.dumps(out, indent=1))
 
 
