@@ -91,19 +91,26 @@ def pmc_traffic(kind: str):
     return (2.0 * fetch + write) * 1024.0, os.path.relpath(files[-1], ROOT)
 
 
-def pmc_mfma_util(kind: str):
-    """Ideal MFMA cycles of `kind` over (duration x clock) from the newest committed
-    profiles/r*/bench_pmc_mfma.json (tools/pmc_mfma.py), or None.  SQ_VALU_MFMA_BUSY_CYCLES is the
-    issued MFMA count x 16 on gfx950, so this restates the kernel time at the clock it ran at
-    (GRBM_GUI_ACTIVE); it is not an independent busy measurement."""
+def pmc_attribution(kind: str):
+    """The newest committed cycle attribution of the forward GEMM (profiles/r*/fwd_dx_pmc_attribution.json,
+    tools/pmc_attr.py over three rocprofv3 SQ / TCC passes): the MFMA pipe's busy fraction of the SIMD
+    cycles, the non-MFMA VALU issue and the rest, and the L2 numbers -- or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "bench_pmc_mfma.json")))
-    if not files or kind not in KIND_MATCH:
+    if kind != "inner_fwd":
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "fwd_dx_pmc_attribution.json")))
+    if not files:
         return None
     with open(files[-1]) as f:
         pmc = json.load(f)
-    vals = [v["mfma_util"] for k, v in pmc.items() if kind_match(kind, k)]
-    return sum(vals) / len(vals) if vals else None
+    fwd = next((v for k, v in pmc.items() if k.startswith("forward (NT_FWD)")), None)
+    if not fwd or "simd_cycles" not in fwd:
+        return None
+    sc = fwd["simd_cycles"]
+    return {"mfma_pipe_busy": sc["mfma_pipe"], "non_mfma_valu_issue": sc["non_mfma_valu_issue"],
+            "rest": 1.0 - sc["mfma_pipe"] - sc["non_mfma_valu_issue"],
+            "l2_hit_rate": fwd.get("l2", {}).get("hit_rate (reads and writes)"),
+            "source": os.path.relpath(files[-1], ROOT)}
 
 
 CONFIGS = {  # name: (hidden, layers, in_dim, coords per GPU, omega0, grid height per GPU or None)
@@ -535,9 +542,10 @@ def main():
                      "flops_per_launch": flops_gemm,
                      "hbm_gbs_at_traffic": (traffic / (kernels[dom]["avg_ms"] * 1e-3) / 1e9)
                      if traffic else None,
-                     # = ideal MFMA cycles / (launch time x the clock it ran at): time x clock, not a
-                     # separate busy counter (pmc_mfma_util)
-                     "mfma_cycles_over_time_x_clock_pmc": pmc_mfma_util(dom) if headline else None},
+                     # the committed cycle attribution of this kernel (tools/pmc_attr.py): MFMA pipe
+                     # busy = SQ_INSTS_MFMA x 16 cycles / 1024 SIMDs over the dispatch's cycles
+                     # (GRBM_GUI_ACTIVE / 8), and the clock it ran at; frac = busy x clock / 2.4 GHz
+                     "pmc_attribution": pmc_attribution(dom) if headline else None},
         # every GEMM kind's spec-peak fraction (the dominant one is `roofline`); head_fwd does the
         # forward GEMM's flops plus the head, loss gradient and head backward
         "gemm_frac_by_kind": {k: kernels[k]["tflops"] / PEAK_BF16_TFLOPS for k in gemm_kinds},

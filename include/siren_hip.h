@@ -418,7 +418,10 @@ enum siren_prof_kind {
 /* tuning knobs for in-process A/B measurement (process-global; 0 = automatic):
  * SIREN_OPT_NT_TILE / SIREN_OPT_TN_TILE = 128 or 256 forces the GEMM tile edge;
  * SIREN_OPT_NT_PIPE = 256x256 NT GEMM K-loop: -1 automatic (4), 0 BK 64 one tile per block,
- * 1 BK 64 persistent double buffer, 4 BK 64 persistent with two wave groups in ping-pong;
+ * 1 BK 64 persistent double buffer, 4 BK 64 persistent with two wave groups in ping-pong; the
+ * plain forward (no head) also takes the one-wave-per-SIMD measurement kernels 5 (128x256 tiles,
+ * the epilogue under the next tile's MFMAs), 6 (256x256, BK 32, 4-stage ring) and 7 (pipe 5's K loop
+ * with the epilogue at the tile's end), bit-identical to 4; other modes take 4;
  * SIREN_OPT_TN_PIPE = -1..4 selects the 256x256 dW K-loop (-1 automatic = 4; 0: BK 64 double
  * buffer, 1: BK 32 4-slot ring, 2: BK 32 5-slot ring, 3: BK 64 ping-pong in 16-MFMA phases,
  * 4: BK 64 ping-pong in 32-MFMA segments);

@@ -1,4 +1,7 @@
-// Forward SineLayer GEMM with the epilogue under the next tile's MFMAs (SIREN_OPT_NT_PIPE 5).
+// Forward SineLayer GEMM with the epilogue under the next tile's MFMAs (SIREN_OPT_NT_PIPE 5), and the
+// same K loop with the epilogue at the tile's end (pipe 7).  MEASUREMENT OPTIONS, not the product:
+// bit-identical to the ping-pong forward but slower (3.05 / 2.83 vs 2.30 ms per 2^20 x 1024^2
+// launch): one wave per SIMD makes the K loop issue-bound.
 //
 //   Y = sin(omega (X W^T + b)),  C = cos(omega (X W^T + b))          -- models.py:114-115
 //

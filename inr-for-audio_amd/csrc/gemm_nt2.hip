@@ -1,4 +1,7 @@
-// Forward SineLayer GEMM, one wave per SIMD on 256x256 tiles (SIREN_OPT_NT_PIPE 6).
+// Forward SineLayer GEMM, one wave per SIMD on 256x256 tiles (SIREN_OPT_NT_PIPE 6).  MEASUREMENT
+// OPTION, not the product: bit-identical to the ping-pong forward, 2.76 vs 2.30 ms (the K loop alone
+// 2.06 vs 1.59: issue-bound with one wave per SIMD, and the 64-B rows split every 128-B line across
+// two K-tiles).  The reasoning it was built on:
 //
 //   Y = sin(omega (X W^T + b)),  C = cos(omega (X W^T + b))          -- models.py:114-115
 //

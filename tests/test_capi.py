@@ -111,9 +111,10 @@ def test_set_option_ranges(lib):
     the defaults restored; SIREN_OPT_NT_QUEUE takes 0 (static walk), 1 (forward modes), 2 (all).
     The product library carries no measurement ablation: SIREN_OPT_NT_DIAG accepts only 0, and
     the retired stagger (5) and prefetch-distance (7) options are rejected; SIREN_OPT_HEAD_FUSE (9)
-    takes 0 or 1; the hand-off fault hook SIREN_OPT_HB_FAULT (10) only 0."""
+    takes 0 or 1; the hand-off fault hook SIREN_OPT_HB_FAULT (10) only 0.  SIREN_OPT_NT_PIPE takes the
+    measurement forwards 5-7 (one wave per SIMD, gemm_nt1.hip / gemm_nt2.hip) besides -1, 0, 1, 4."""
     bad = 1003  # SIREN_ERR_CONFIG
-    for opt, good, wrong in ((0, (0, 128, 256), (64,)), (1, (0, 128, 256), (512,)), (2, (-1, 0, 1, 4), (2, 3, 5, 7, -2)),
+    for opt, good, wrong in ((0, (0, 128, 256), (64,)), (1, (0, 128, 256), (512,)), (2, (-1, 0, 1, 4, 5, 6, 7), (2, 3, 8, -2)),
                              (3, (-1, 4), (5,)), (4, (0, 16), (-1,)), (5, (), (0, 1)),
                              (6, (0,), (1, 4, 512, 1024, 2, 8)), (7, (), (1, 2)), (8, (0, 1, 2), (3, -1)),
                              (9, (0, 1), (2, -1)), (10, (0,), (1, 1 << 8, -1))):
