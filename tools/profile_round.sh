@@ -5,6 +5,7 @@
 #   bench_pmc_hbm.json      FETCH_SIZE and WRITE_SIZE, each in its own --pmc pass
 #   bench_pmc_mfma.json     SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE: MFMA utilisation per kernel
 #   bench_pmc_lds.json      SQ_LDS_IDX_ACTIVE / _BANK_CONFLICT / _UNALIGNED_STALL + GRBM_GUI_ACTIVE
+#   fwd_dx_pmc_attribution.json  the forward / dX GEMMs' cycle attribution (tools/pmc_attr.py: 3 SQ / TCC passes)
 #   bench_cfg{3,4,5}.json   the other BASELINE configs' bench lines; trace_cfg{3,4,5}/ their
 #                           rocprofv3 --kernel-trace --stats
 # Every GPU step has its own time limit and the steps are chained with &&.
@@ -27,6 +28,11 @@ timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --out
   python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_mfma.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_lds" -o run -- \
   python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_lds.log" 2>&1 &&
+AB="python3 $ROOT/tools/ab_bench.py --libs base=inr-for-audio_amd/libsiren_hip.so --only fwd,dx --rounds 2 --reps 3" &&
+(cd "$ROOT" && timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MFMA GRBM_GUI_ACTIVE --output-format csv -d "$OUT/attr_a" -o run -- $AB > "$OUT/attr_a.log" 2>&1) &&
+(cd "$ROOT" && timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE --output-format csv -d "$OUT/attr_b" -o run -- $AB > "$OUT/attr_b.log" 2>&1) &&
+(cd "$ROOT" && timeout -k 10 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/attr_c" -o run -- $AB > "$OUT/attr_c.log" 2>&1) &&
+python3 "$ROOT/tools/pmc_attr.py" "$OUT/fwd_dx_pmc_attribution.json" "$OUT/attr_a" "$OUT/attr_b" "$OUT/attr_c" &&
 python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_lds.json" "$OUT/pmc_lds" &&
 python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_hbm.json" "$OUT/pmc_fetch" "$OUT/pmc_write" &&
 python3 "$ROOT/tools/pmc_mfma.py" "$OUT/bench_pmc_mfma.json" "$OUT/pmc_mfma" &&
