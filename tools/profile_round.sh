@@ -19,15 +19,15 @@ cd /tmp && export TMPDIR=/tmp
 python3 "$ROOT/__graft_entry__.py"
 timeout -k 10 400 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/trace.log" 2>&1 &&
+  python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-recon-snr > "$OUT/trace.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1 &&
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-recon-snr > "$OUT/pmc_fetch.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1 &&
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-recon-snr > "$OUT/pmc_write.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_mfma" -o run -- \
-  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_mfma.log" 2>&1 &&
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-recon-snr > "$OUT/pmc_mfma.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_lds" -o run -- \
-  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_lds.log" 2>&1 &&
+  python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-recon-snr > "$OUT/pmc_lds.log" 2>&1 &&
 AB="python3 $ROOT/tools/ab_bench.py --libs base=inr-for-audio_amd/libsiren_hip.so --only fwd,dx --rounds 2 --reps 3" &&
 (cd "$ROOT" && timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MFMA GRBM_GUI_ACTIVE --output-format csv -d "$OUT/attr_a" -o run -- $AB > "$OUT/attr_a.log" 2>&1) &&
 (cd "$ROOT" && timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_SMEM GRBM_GUI_ACTIVE --output-format csv -d "$OUT/attr_b" -o run -- $AB > "$OUT/attr_b.log" 2>&1) &&
@@ -40,6 +40,6 @@ for c in cfg3 cfg4 cfg5; do
   # every config line carries its CPU baseline (cfg3 / cfg4: the SIREN port at the job's thread share)
   timeout -k 10 300 python3 "$ROOT/bench.py" --config $c > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" &&
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$c" -o run -- \
-    python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/trace_$c.log" 2>&1 || exit 3
+    python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-recon-snr > "$OUT/trace_$c.log" 2>&1 || exit 3
 done
 echo "profile $TAG done"
