@@ -746,7 +746,7 @@ int siren_set_option(int32_t option, int32_t value) {
       gemm_nt_set_grid_cap(value);
       return SIREN_OK;
     case SIREN_OPT_NT_DIAG:
-      if (value < 0 || (value & ~(1 | 4 | 8 | 512 | 1024 | 2048 | (0xff << 16)))) return SIREN_ERR_CONFIG;
+      if (value < 0 || (value & ~(1 | 4 | 8 | 512 | 1024 | 2048))) return SIREN_ERR_CONFIG;
       return gemm_nt_set_diag(value) ? SIREN_OK : SIREN_ERR_CONFIG;
     case SIREN_OPT_NT_QUEUE:
       if (value < 0 || value > 2) return SIREN_ERR_CONFIG;

@@ -182,10 +182,6 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // 1 X from the first 4 row bands (L2-resident X), 4 W from column tile 0, 8 X from the first 256
   // row bands (128 MB: beyond L2, inside the Infinity Cache), 512 no tiles, 1024 no epilogue
   const int diag = (SIREN_DIAG_ON && !(Cfg::PP && QUEUE)) ? p.diag : 0;
-  // diag bits 16-23 (SIREN_DIAG builds, plain forward, ping-pong): elements added to the row stride
-  // of X and of Y / C (a padded activation layout; measurement only -- the product is dense)
-  const int ldpad = (SIREN_DIAG_ON && Cfg::PP && MODE == NT_FWD && !HEAD) ? (diag >> 16) & 0xff : 0;
-  const int ldx = K + ldpad, ldy = N + ldpad;
   const int my_tiles = (diag & 512) ? 0 : (ntiles - bp + G - 1) / G;
   // Dynamic tile queue (ping-pong K-loop, NtParams::tileq).  With the static walk the four
   // blocks that share a row band of X drift apart over the launch and X is fetched ~1.6x from
@@ -632,7 +628,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       for (int j = 0; j < SM; ++j) hp[j] = 0.f;
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
-        const size_t rowoff = (size_t)(mrow0 + j * 16) * ldy;
+        const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
         uint4 yp[SN / 2], cpk[SN / 2], epk[SN / 2];
 #pragma unroll
         for (int q = 0; q < SN / 2; ++q) {
@@ -891,8 +887,6 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     int urow[4][2];
     unsigned pdst[4][2];
     const unsigned lane_src = (unsigned)(((lane >> 3) * K + stage_swz<BK>(lane >> 3, lane & 7) * 8) * 2);
-    const unsigned lane_src_x = SIREN_DIAG_ON ? (unsigned)(((lane >> 3) * ldx + stage_swz<BK>(lane >> 3, lane & 7) * 8) * 2)
-                                              : lane_src;
 #pragma unroll
     for (int pc = 0; pc < 4; ++pc)
 #pragma unroll
@@ -900,7 +894,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         const int pr0 = (2 * wave + j) * 8, hf = pc >> 1;
         const int lr0 = (pc & 1) ? (pr0 >> 6) * 128 + (pr0 & 63) + 64 * hf
                                  : (pr0 >> 5) * 64 + (pr0 & 31) + 32 * hf;
-        urow[pc][j] = lr0 * ((pc & 1) ? ldx : K) * 2;
+        urow[pc][j] = lr0 * K * 2;
         pdst[pc][j] = ((pc & 1) ? 0u : (unsigned)Cfg::XBYTES) + (unsigned)(lr0 * ROWB);
       }
     // operand bases of the current tile (0) and the next one (1), set once per tile:
@@ -940,7 +934,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       auto bases = [&](int g, const h16*& xb, const h16*& wb) {
         int m0, n0;
         tile_of(g, m0, n0);
-        xb = p.X + (size_t)xrow(m0) * ldx;
+        xb = p.X + (size_t)xrow(m0) * K;
         wb = p.W + (size_t)((diag & 4) ? 0 : n0) * K;  // diag bit 2: one W column tile (L2-resident W)
       };
       bases(g_cur, x0, w0);
@@ -952,7 +946,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       const char* dst = smem + slot * Cfg::STAGE;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        glds16_asm_s((PC & 1) ? lane_src_x : lane_src, (const char*)src + urow[PC][j], lds_addr(dst + pdst[PC][j]));
+        glds16_asm_s(lane_src, (const char*)src + urow[PC][j], lds_addr(dst + pdst[PC][j]));
     };
     h16x8 xf[4][2], wf0[2][2], wf1[2][2];
     auto rd_w = [&](h16x8 (&wf)[2][2], const char* ws, int n_off) {
