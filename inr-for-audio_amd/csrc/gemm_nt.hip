@@ -45,13 +45,6 @@
 #define SIREN_SNAKE0_EB 2
 #endif
 
-// forward (NT_FWD, no head), ping-pong, N = 1024 (4 column tiles per row band): wave 0 of every block
-// prefetches into L2 its quarter of the band's X rows for K-tile kt + SIREN_NT_XPF while the group
-// computes K-tile kt (one dword per lane per K-step; 0 = off, the product)
-#ifndef SIREN_NT_XPF
-#define SIREN_NT_XPF 0
-#endif
-
 #ifdef SIREN_DIAG
 #define SIREN_DIAG_ON 1
 #else
@@ -107,8 +100,7 @@ struct NtLds {
   static constexpr int A = HW + (HEAD ? Cfg::VEC : 0);
   static constexpr int IA = A + (nt_is_snake_fwd(MODE) ? Cfg::VEC : 0);   // Snake 1/a, divided once
   static constexpr int QS = IA + (nt_is_snake_fwd(MODE) ? Cfg::VEC : 0);  // dynamic tile queue: 2 tile ids
-  static constexpr int PF = QS + 16;  // X prefetch landing (SIREN_NT_XPF; 256 B, never read)
-  static constexpr int SIZE = PF + (SIREN_NT_XPF ? 256 : 0);
+  static constexpr int SIZE = QS + 16;
   static_assert(SIZE <= 160 * 1024, "LDS");
 };
 
@@ -908,7 +900,6 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     // operand bases of the current tile (0) and the next one (1), set once per tile:
     // no division or 64-bit product in the per-phase scalar work
     const h16 *x0 = p.X, *x1 = p.X, *w0 = p.W, *w1 = p.W;
-    int c0 = 0, c1 = 0;  // column tile index of the current / next tile (X prefetch rows)
     // This block's current and next tile (global ids); the next one exists while it lies in
     // [g_lo, g_lim).  Static walk: bp, bp + G, ...  Queue: shard s = blockIdx % 8 (one XCD under
     // round-robin dispatch -- speed only, any placement is correct) pulls tiles
@@ -940,15 +931,14 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         // queue: the pull tile_end(ti - 1) left in the slot
         g_next = dyn ? __builtin_amdgcn_readfirstlane(qslot[0]) : g_next + G;
       }
-      auto bases = [&](int g, const h16*& xb, const h16*& wb, int& c) {
+      auto bases = [&](int g, const h16*& xb, const h16*& wb) {
         int m0, n0;
         tile_of(g, m0, n0);
         xb = p.X + (size_t)xrow(m0) * K;
         wb = p.W + (size_t)((diag & 4) ? 0 : n0) * K;  // diag bit 2: one W column tile (L2-resident W)
-        c = n0 / BN;
       };
-      bases(g_cur, x0, w0, c0);
-      bases(in_range(g_next) ? g_next : g_cur, x1, w1, c1);
+      bases(g_cur, x0, w0);
+      bases(in_range(g_next) ? g_next : g_cur, x1, w1);
     };
     auto issue = [&](int sel, int kt, int slot, auto pcc) {
       constexpr int PC = decltype(pcc)::value;
@@ -1014,19 +1004,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
         for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    constexpr int XPF = (SIREN_NT_XPF > 0 && MODE == NT_FWD && !HEAD) ? 1 : 0;
-    // X prefetch for K-tile kt + SIREN_NT_XPF (of this tile or the next): rows c*64 .. c*64+63 of the
-    // band, one 128-B line per lane (N = 1024 only: 4 column tiles share the band)
-    auto xpf = [&](int kt) {
-      int kp = kt + SIREN_NT_XPF;
-      const bool nx = kp >= nk;
-      kp -= nx ? nk : 0;
-      const h16* xb = nx ? x1 : x0;
-      const int c = nx ? c1 : c0;
-      glds4_asm((const char*)xb + ((size_t)(c * 64 + lane) * K + (size_t)kp * BK) * 2, lds_addr(smem + Lay::PF));
-    };
-    pingpong_tiles_pf<epilogue_stores<Cfg, MODE>(), 0xB, XPF>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles,
-                                                              tile_end, more, xpf, XPF && wave == 0 && tiles_n == 4);
+    pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles,
+                                                       tile_end, more);
   } else {
     mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
         my_tiles, K / BK, acc, stage, frags, [&](int ti) { pre(bp + ti * G); },

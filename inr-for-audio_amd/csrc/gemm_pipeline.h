@@ -272,34 +272,21 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// Optional prefetch hook (PFN > 0, a measurement build): a wave with `pfw` issues PFN extra
-// vector-memory instructions (`pf(kt)`) in phase 0 of every K-step, right after the phase's pieces
-// (and once in the prologue, at the same place of the virtual K-step -1, so every K-step sees the
-// same pattern); its counted waits allow them: phase 0 waits past pf(kt - 1) and pf(kt) (+2 PFN),
-// phases 1 and 3 past pf(kt) (+PFN).  PFN = 0 is the product schedule, unchanged.
-template <int E, int WAITMASK, int PFN = 0, class IssueFn, class ReadFn, class MmaFn, class SetFn, class EndFn,
-          class MoreFn, class PfFn>
-__device__ __forceinline__ void pingpong_tiles_pf(bool any, int nk, int grp, IssueFn&& issue,
-                                                   ReadFn&& read, MmaFn&& mma, SetFn&& set_tiles,
-                                                   EndFn&& tile_end, MoreFn&& more, PfFn&& pf, bool pfw) {
-  static_assert(E >= 0 && 8 + E + 2 * PFN < 64, "vmcnt immediate");
+template <int E, int WAITMASK, class IssueFn, class ReadFn, class MmaFn, class SetFn, class EndFn,
+          class MoreFn>
+__device__ __forceinline__ void pingpong_tiles(bool any, int nk, int grp, IssueFn&& issue,
+                                                ReadFn&& read, MmaFn&& mma, SetFn&& set_tiles,
+                                                EndFn&& tile_end, MoreFn&& more) {
+  static_assert(E >= 0 && 8 + E < 64, "vmcnt immediate");
   if (!any || nk <= 0) return;
   set_tiles(0);
   issue(0, 0, 0, phase_t<0>{});
   issue(0, 0, 0, phase_t<1>{});
   issue(0, 0, 0, phase_t<2>{});
-  if constexpr (PFN > 0) {
-    if (pfw) pf(-1);
-  }
   issue(0, 0, 0, phase_t<3>{});
   issue(0, 1, 1, phase_t<0>{});
   issue(0, 1, 1, phase_t<1>{});
-  if constexpr (PFN > 0) {
-    if (pfw) wait_vmcnt<8 + PFN>();
-    else wait_vmcnt<8>();
-  } else {
-    wait_vmcnt<8>();  // this wave's share of K-tile 0's pieces 0, 1 has landed
-  }
+  wait_vmcnt<8>();  // this wave's share of K-tile 0's pieces 0, 1 has landed
   wait_lgkm0();
   pp_barrier();           // ... every wave's
   if (grp) pp_barrier();  // group 1 runs one barrier behind
@@ -317,18 +304,7 @@ __device__ __forceinline__ void pingpong_tiles_pf(bool any, int nk, int grp, Iss
       read(ph, slot);
       if constexpr (PH < 2) issue(sa, ka, slot ^ 1, phase_t<PH + 2>{});
       else issue(sb, kb, slot, phase_t<PH - 2>{});
-      if constexpr (PFN > 0 && PH == 0) {
-        if (pfw) pf(kt);
-      }
-      if constexpr (((WAITMASK >> PH) & 1) != 0) {
-        constexpr int BASE = RELAXED ? 8 + E : 8;
-        if constexpr (PFN > 0) {
-          if (pfw) wait_vmcnt<BASE + (PH == 0 ? 2 * PFN : PFN)>();
-          else wait_vmcnt<BASE>();
-        } else {
-          wait_vmcnt<BASE>();
-        }
-      }
+      if constexpr (((WAITMASK >> PH) & 1) != 0) wait_vmcnt<RELAXED ? 8 + E : 8>();
       pp_barrier();
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
@@ -354,12 +330,6 @@ __device__ __forceinline__ void pingpong_tiles_pf(bool any, int nk, int grp, Iss
     if (grp == 1) pp_barrier();  // group 1 one barrier behind again
   }
   wait_vmcnt<0>();
-}
-
-template <int E, int WAITMASK, class IssueFn, class ReadFn, class MmaFn, class SetFn, class EndFn, class MoreFn>
-__device__ __forceinline__ void pingpong_tiles(bool any, int nk, int grp, IssueFn&& issue, ReadFn&& read,
-                                                MmaFn&& mma, SetFn&& set_tiles, EndFn&& tile_end, MoreFn&& more) {
-  pingpong_tiles_pf<E, WAITMASK, 0>(any, nk, grp, issue, read, mma, set_tiles, tile_end, more, [](int) {}, false);
 }
 
 // Two-segment variant (one tile per block, e.g. the split-K dW GEMM): a K-tile is two segments

@@ -92,21 +92,6 @@ __device__ __forceinline__ void glds16_asm_s(unsigned voff, const void* sbase, u
       : "memory");
 }
 
-// The same with one dword per lane: 64 lines touched (an L2 prefetch whose data lands in a 256-B
-// LDS scratch that is never read)
-__device__ __forceinline__ void glds4_asm(const void* gsrc, unsigned lds_byte) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dword %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_byte))
-      : "memory");
-}
-
 // First SineLayer pre-activation z = t W0^T + b0 rounded as torch's CPU addmm (K=1: one fma;
 // K=2: fma(t1, w1, t0*w0) + b) -- models.py:114-115 with is_first.
 __device__ __forceinline__ float first_preact(int in_dim, float t0, float t1, float w0, float w1, float b) {
