@@ -19,7 +19,8 @@
 // Tiles: 256x256 with 8 waves (2x4, each 128x64 = 8x4 v_mfma_f32_16x16x32_f16 tiles),
 // PERSISTENT: one block per CU walks its tiles and the double-buffered LDS ring runs across
 // tile boundaries; the default K-loop is the ping-pong of two wave groups one barrier apart
-// (gemm_pipeline.h pingpong_tiles).  A 128x128 / 4-wave config (one tile per block) serves
+// (gemm_pipeline.h pingpong2_tiles: two 32-MFMA segments per K-step).  A 128x128 / 4-wave config
+// (one tile per block) serves
 // grids too small for 256x256.  Operands are staged HBM->LDS by LDS-DMA (global_load_lds_dwordx4
 // from inline asm), with an XOR swizzle on the SOURCE address so that the ds_read_b128 fragment
 // reads are bank-conflict free (cdna_hip_programming.md §5.4 rule 21 / T2).
@@ -43,6 +44,13 @@
 #endif
 #ifndef SIREN_SNAKE0_EB
 #define SIREN_SNAKE0_EB 2
+#endif
+
+// ping-pong NT kernels: the two-segment K-step (gemm_pipeline.h pingpong2_tiles, 4 barriers per K-step;
+// round 5: forward 2.269 -> 2.201 ms, fused last layer 2.401 -> 2.338, dX0 1.963 -> 1.924, dX 2.168 ->
+// 2.156, bit-identical; profiles/r18/ab_seg2.json); 0 = the four-phase K-step (pingpong_tiles)
+#ifndef SIREN_NT_SEG2
+#define SIREN_NT_SEG2 1
 #endif
 
 #ifdef SIREN_DIAG
@@ -1004,8 +1012,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
         for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
-    pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles,
-                                                       tile_end, more);
+    if constexpr (SIREN_NT_SEG2 != 0)
+      pingpong2_tiles<epilogue_stores<Cfg, MODE>()>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles, tile_end,
+                                                     more);
+    else
+      pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles,
+                                                         tile_end, more);
   } else {
     mfma_pipeline_tiles<Cfg::S, BK / 32, Cfg::XINSTR + Cfg::WINSTR, SN, SM, epilogue_stores<Cfg, MODE>()>(
         my_tiles, K / BK, acc, stage, frags, [&](int ti) { pre(bp + ti * G); },

@@ -332,6 +332,75 @@ __device__ __forceinline__ void pingpong_tiles(bool any, int nk, int grp, IssueF
   wait_vmcnt<0>();
 }
 
+// Persistent two-segment variant of pingpong_tiles (a measurement option of the NT kernels): a K-step
+// is two segments of 32 MFMAs -- segment 0 = phases 0, 1 (reads pieces 0..2, issues piece 3 of K-tile
+// kt + 1), segment 1 = phases 2, 3 (reads piece 3, issues pieces 0..2 of kt + 2) -- so 4 barriers per
+// K-step instead of 8.  Each segment retires its own reads (lgkmcnt(0)) before its first barrier: the
+// other group, one barrier behind, overwrites those pieces one barrier later (pingpong2_one_tile's
+// rule).  Every wait is vmcnt(8) (8 + E in a tile's first K-step after an epilogue): the pieces
+// issued in the two segments since the awaited ones.
+template <int E, class IssueFn, class ReadFn, class MmaFn, class SetFn, class EndFn, class MoreFn>
+__device__ __forceinline__ void pingpong2_tiles(bool any, int nk, int grp, IssueFn&& issue, ReadFn&& read,
+                                                MmaFn&& mma, SetFn&& set_tiles, EndFn&& tile_end, MoreFn&& more) {
+  static_assert(E >= 0 && 8 + E < 64, "vmcnt immediate");
+  if (!any || nk <= 0) return;
+  set_tiles(0);
+  issue(0, 0, 0, phase_t<0>{});
+  issue(0, 0, 0, phase_t<1>{});
+  issue(0, 0, 0, phase_t<2>{});
+  issue(0, 0, 0, phase_t<3>{});
+  issue(0, 1, 1, phase_t<0>{});
+  issue(0, 1, 1, phase_t<1>{});
+  issue(0, 1, 1, phase_t<2>{});
+  wait_vmcnt<8>();  // K-tile 0's pieces 0..2 (and the older ones) have landed
+  wait_lgkm0();
+  pp_barrier();
+  if (grp) pp_barrier();  // group 1 runs one barrier behind
+  auto kstep = [&](int kt, auto relaxed) {
+    constexpr bool RELAXED = decltype(relaxed)::value;
+    const int slot = kt & 1;
+    int ka = kt + 1, kb = kt + 2;
+    const int sa = ka >= nk, sb = kb >= nk;
+    ka -= sa ? nk : 0;
+    kb -= sb ? nk : 0;
+    auto segment = [&](auto sg) {
+      constexpr int SG = decltype(sg)::value;
+      read(phase_t<2 * SG>{}, slot);
+      read(phase_t<2 * SG + 1>{}, slot);
+      if constexpr (SG == 0) {
+        issue(sa, ka, slot ^ 1, phase_t<3>{});
+      } else {
+        issue(sb, kb, slot, phase_t<0>{});
+        issue(sb, kb, slot, phase_t<1>{});
+        issue(sb, kb, slot, phase_t<2>{});
+      }
+      wait_vmcnt<RELAXED ? 8 + E : 8>();
+      wait_lgkm0();
+      pp_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      mma(phase_t<2 * SG>{});
+      mma(phase_t<2 * SG + 1>{});
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    };
+    segment(phase_t<0>{});
+    segment(phase_t<1>{});
+  };
+  for (int ti = 0;; ++ti) {
+    if (ti == 0) kstep(0, std::false_type{});
+    else kstep(0, std::true_type{});
+    for (int kt = 1; kt < nk; ++kt) kstep(kt, std::false_type{});
+    if (grp == 0) pp_barrier();  // meet group 1's last barrier: aligned
+    tile_end(ti);
+    const bool next = more(ti);
+    if (!next) break;
+    set_tiles(ti + 1);
+    if (grp == 1) pp_barrier();  // group 1 one barrier behind again
+  }
+  wait_vmcnt<0>();
+}
+
 // Two-segment variant (one tile per block, e.g. the split-K dW GEMM): a K-tile is two segments
 // of 32 MFMAs instead of four phases of 16, halving the barriers.  Segment A reads pieces
 // 0 .. NA-1 of K-tile u and issues pieces NA..3 of u+1 into the other slot; segment B reads
