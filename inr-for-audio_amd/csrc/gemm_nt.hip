@@ -72,7 +72,7 @@ __device__ __forceinline__ int stage_swz(int r, int c) {
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int S_, bool PP_ = false>
 struct NtCfg {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, S = S_;
-  static constexpr bool PP = PP_;  // ping-pong K-loop (gemm_pipeline.h pingpong_tiles)
+  static constexpr bool PP = PP_;  // ping-pong K-loop (gemm_pipeline.h pingpong2_tiles / pingpong_tiles)
   static constexpr int WM = WM_, WN = WN_, NWAVES = WM_ * WN_, THREADS = 64 * NWAVES;
   static constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   static constexpr int SM = TM / 16, SN = TN / 16;  // 16x16 MFMA tiles per wave
@@ -1163,7 +1163,7 @@ static hipError_t dispatch_act(int mode, bool head, const NtParams& p, hipStream
 }
 
 // tile override for A/B measurement: 0 = auto, 128 or 256; pipe (256x256): 0 = BK 64, one
-// tile per block; 1 = BK 64 persistent; 4 = BK 64 persistent ping-pong (pingpong_tiles)
+// tile per block; 1 = BK 64 persistent; 4 = BK 64 persistent ping-pong (pingpong2_tiles)
 static int g_nt_tile = 0;
 static int g_nt_pipe = -1;  // -1: automatic = ping-pong 4 for every mode (kernel_bench r06)
 static bool nt_pp() { return g_nt_pipe < 0 || (g_nt_pipe >= 4 && g_nt_pipe <= 7); }

@@ -332,7 +332,7 @@ __device__ __forceinline__ void pingpong_tiles(bool any, int nk, int grp, IssueF
   wait_vmcnt<0>();
 }
 
-// Persistent two-segment variant of pingpong_tiles (a measurement option of the NT kernels): a K-step
+// Persistent two-segment variant of pingpong_tiles (the NT kernels' default, SIREN_NT_SEG2): a K-step
 // is two segments of 32 MFMAs -- segment 0 = phases 0, 1 (reads pieces 0..2, issues piece 3 of K-tile
 // kt + 1), segment 1 = phases 2, 3 (reads piece 3, issues pieces 0..2 of kt + 2) -- so 4 barriers per
 // K-step instead of 8.  Each segment retires its own reads (lgkmcnt(0)) before its first barrier: the

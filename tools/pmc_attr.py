@@ -62,10 +62,13 @@ def main():
     for name, ctrs in per.items():
         m = NT.search(name)
         m1 = ONE.search(name)
-        if not m and not m1:
+        tn = "gemm_tn_kernel<" in name
+        if not m and not m1 and not tn:
             continue
         a = {c: sum(v) / len(v) for c, v in ctrs.items()}
-        if m1:
+        if tn:
+            key = "dW (split-K TN)"
+        elif m1:
             key = f"forward one wave per SIMD (pipe 5, NK {m1.group(1)}, diag {m1.group(2)})"
         else:
             key = f"{MODES.get(m.group(2), 'mode ' + m.group(2))}{' +head' if m.group(3) == 'true' else ''}" \
