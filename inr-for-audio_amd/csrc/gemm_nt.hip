@@ -685,6 +685,14 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           cpk[pp] = swap16_pair(cs[0], cs[1]);
           if constexpr (MODE == NT_FWD_SNAKE) epk[pp] = swap16_pair(es[0], es[1]);
         }
+        if (SIREN_DIAG_ON && (diag & 2048)) {  // diag bit 11: the epilogue without its stores (timing only)
+          unsigned keep = 0;
+#pragma unroll
+          for (int pp = 0; pp < SN / 2; ++pp)
+            keep ^= yp[pp].x ^ yp[pp].y ^ yp[pp].z ^ yp[pp].w ^ cpk[pp].x ^ cpk[pp].y ^ cpk[pp].z ^ cpk[pp].w;
+          asm volatile("" ::"v"(keep));
+          continue;
+        }
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
           st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
