@@ -53,6 +53,10 @@
 #define SIREN_NT_SEG2 1
 #endif
 
+#ifndef SIREN_NT_STNT
+#define SIREN_NT_STNT 0
+#endif
+
 #ifdef SIREN_DIAG
 #define SIREN_DIAG_ON 1
 #else
@@ -108,7 +112,10 @@ struct NtLds {
   static constexpr int A = HW + (HEAD ? Cfg::VEC : 0);
   static constexpr int IA = A + (nt_is_snake_fwd(MODE) ? Cfg::VEC : 0);   // Snake 1/a, divided once
   static constexpr int QS = IA + (nt_is_snake_fwd(MODE) ? Cfg::VEC : 0);  // dynamic tile queue: 2 tile ids
-  static constexpr int SIZE = QS + 16;
+  // plain forward and dX, ping-pong config: a 2-KiB scratch per wave that turns the epilogue's 16-row x
+  // 64-B store pieces into whole 128-B lines (the 128x128 config keeps two blocks per CU without it)
+  static constexpr int ST = QS + 16;
+  static constexpr int SIZE = ST + ((Cfg::PP && (MODE == NT_FWD || MODE == NT_DX) && !HEAD) ? Cfg::NWAVES * 2048 : 0);
   static_assert(SIZE <= 160 * 1024, "LDS");
 };
 
@@ -263,6 +270,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // swap16_pair, this lane's piece starting at column ncol + 32p + swap16_col(lane).
   float* red = (float*)(smem + Cfg::RING);
   auto st16 = [&](h16* dst, uint4 v) { *(uint4*)dst = v; };
+  // the whole-line stores (plain forward, dX); SIREN_NT_STNT (measurement): non-temporal
+  auto stl = [&](h16* dst, uint4 v) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    if constexpr (SIREN_NT_STNT != 0) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (u32x4*)dst);
+    else *(uint4*)dst = v;
+  };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
   float* bias_lds = (float*)(smem + Lay::BIAS);
@@ -693,6 +706,34 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           asm volatile("" ::"v"(keep));
           continue;
         }
+        if constexpr (Cfg::PP && MODE == NT_FWD && !HEAD) {
+          // Whole 128-B lines per store: the wave's 16-row x 64-column piece of Y (then of C) goes
+          // through its 2-KiB LDS scratch (16-B chunks XOR-swizzled by row: conflict-free both ways),
+          // and each store writes rows 8q .. 8q+7 as 8 lanes x 16 B per row.  Same bytes and store
+          // count as 16 rows x 64 B, but no half-line writes: forward -4.6%, cfg4 -6.5% (static walk,
+          // profiles/r19/ab_full_lines.json).  Same-wave LDS accesses complete in order, so the reads
+          // see this wave's writes and the next output's writes follow the reads.
+          char* sc = smem + Lay::ST + wave * 2048;
+          const int pr = lane & 15, pc = swap16_col(lane) >> 3;  // this lane's piece: row, 16-B chunk
+          const int qr = lane >> 3, qc = lane & 7;                // line layout: row (+ 8 q), chunk
+          const size_t fbase = (size_t)(mrow0 - pr + j * 16 + qr) * N + (n0 + wn * TN) + qc * 8;
+          auto lines = [&](h16* out, const uint4 (&v)[SN / 2]) {
+#pragma unroll
+            for (int pp = 0; pp < SN / 2; ++pp) {
+              const int c = pp * 4 + pc;
+              *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = v[pp];
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int r = qr + 8 * q;
+              stl(out + fbase + (size_t)(8 * q) * N, *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4)));
+            }
+          };
+          static_assert(SN == 4, "a wave's row piece is one 128-B line");
+          lines(p.Y, yp);
+          lines(p.C, cpk);
+          continue;
+        }
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
           st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
@@ -836,6 +877,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             t0 = t_in[j][0];
             t1 = t_in[j][1];
           }
+          uint4 dzq[SN / 2];  // NT_DX with whole-line stores: this row piece's two 16-B pieces
 #pragma unroll
           for (int pp = 0; pp < SN / 2; ++pp) {
             uint2 cpu[2];
@@ -859,7 +901,25 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               });
               dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
             }
-            if constexpr (MODE == NT_DX) st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+            if constexpr (MODE == NT_DX && Cfg::PP) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
+            else if constexpr (MODE == NT_DX) st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+          }
+          if constexpr (MODE == NT_DX && Cfg::PP) {
+            // whole 128-B dZ lines per store through the wave's LDS scratch (as the forward's Y / C)
+            char* sc = smem + Lay::ST + wave * 2048;
+            const int pr = lane & 15, pc = swap16_col(lane) >> 3;
+            const int qr = lane >> 3, qc = lane & 7;
+#pragma unroll
+            for (int pp = 0; pp < SN / 2; ++pp) {
+              const int c = pp * 4 + pc;
+              *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = dzq[pp];
+            }
+            const size_t fbase = (size_t)(mrow0 - pr + j * 16 + qr) * N + (n0 + wn * TN) + qc * 8;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int r = qr + 8 * q;
+              stl(p.dZ + fbase + (size_t)(8 * q) * N, *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4)));
+            }
           }
         }
 #pragma unroll
