@@ -53,8 +53,13 @@
 #define SIREN_NT_SEG2 1
 #endif
 
+#ifndef SIREN_NT_EARLY  // measurement: gemm_pipeline.h pingpong2_tiles EARLY
+#define SIREN_NT_EARLY 0
+#endif
+// whole-line epilogue stores as non-temporal (global_store ... nt): cfg4 forward -6.0%, dX -1.3%, cfg2
+// within 0.2% (profiles/r19/ab_full_lines.json u26); 0 = plain stores
 #ifndef SIREN_NT_STNT
-#define SIREN_NT_STNT 0
+#define SIREN_NT_STNT 1
 #endif
 
 #ifdef SIREN_DIAG
@@ -270,7 +275,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // swap16_pair, this lane's piece starting at column ncol + 32p + swap16_col(lane).
   float* red = (float*)(smem + Cfg::RING);
   auto st16 = [&](h16* dst, uint4 v) { *(uint4*)dst = v; };
-  // the whole-line stores (plain forward, dX); SIREN_NT_STNT (measurement): non-temporal
+  // the whole-line stores (plain forward, dX): non-temporal (SIREN_NT_STNT)
   auto stl = [&](h16* dst, uint4 v) {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     if constexpr (SIREN_NT_STNT != 0) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (u32x4*)dst);
@@ -1081,8 +1086,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
     if constexpr (SIREN_NT_SEG2 != 0)
-      pingpong2_tiles<epilogue_stores<Cfg, MODE>()>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles, tile_end,
-                                                     more);
+      pingpong2_tiles<epilogue_stores<Cfg, MODE>(), SIREN_NT_EARLY != 0>(in_range(g_cur), nk, wm, issue, read, mma,
+                                                                          set_tiles, tile_end, more);
     else
       pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles,
                                                          tile_end, more);

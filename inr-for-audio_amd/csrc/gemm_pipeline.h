@@ -339,7 +339,12 @@ __device__ __forceinline__ void pingpong_tiles(bool any, int nk, int grp, IssueF
 // other group, one barrier behind, overwrites those pieces one barrier later (pingpong2_one_tile's
 // rule).  Every wait is vmcnt(8) (8 + E in a tile's first K-step after an epilogue): the pieces
 // issued in the two segments since the awaited ones.
-template <int E, class IssueFn, class ReadFn, class MmaFn, class SetFn, class EndFn, class MoreFn>
+// EARLY (SIREN_NT_EARLY, measurement): piece 3 of the next tile's K-tile 1 is issued at the tile end,
+// before the epilogue's stores (slot 1 is free once both groups are aligned there), instead of in the
+// next tile's first K-step; the prologue issues it for the first tile the same way.  The first wait
+// that sits behind the stores then moves from K-step 1 segment 0 to K-step 1 segment 1 (segment 0 of
+// K-step 1 waits with 8 + E after an epilogue, and K-step 0 segment 0 issues nothing).
+template <int E, bool EARLY, class IssueFn, class ReadFn, class MmaFn, class SetFn, class EndFn, class MoreFn>
 __device__ __forceinline__ void pingpong2_tiles(bool any, int nk, int grp, IssueFn&& issue, ReadFn&& read,
                                                 MmaFn&& mma, SetFn&& set_tiles, EndFn&& tile_end, MoreFn&& more) {
   static_assert(E >= 0 && 8 + E < 64, "vmcnt immediate");
@@ -352,12 +357,19 @@ __device__ __forceinline__ void pingpong2_tiles(bool any, int nk, int grp, Issue
   issue(0, 1, 1, phase_t<0>{});
   issue(0, 1, 1, phase_t<1>{});
   issue(0, 1, 1, phase_t<2>{});
-  wait_vmcnt<8>();  // K-tile 0's pieces 0..2 (and the older ones) have landed
+  if constexpr (EARLY) {
+    issue(0, 1, 1, phase_t<3>{});
+    wait_vmcnt<10>();  // K-tile 0's pieces 0..2 have landed (K0 p3, K1 p0..3 younger)
+  } else {
+    wait_vmcnt<8>();  // K-tile 0's pieces 0..2 (and the older ones) have landed
+  }
   wait_lgkm0();
   pp_barrier();
   if (grp) pp_barrier();  // group 1 runs one barrier behind
-  auto kstep = [&](int kt, auto relaxed) {
-    constexpr bool RELAXED = decltype(relaxed)::value;
+  // RELAXED: both segments wait past an epilogue's E stores; RELAXED_A: segment 0 only (EARLY, K-step 1)
+  auto kstep = [&](int kt, auto relaxed, auto relaxed_a, auto skip_a) {
+    constexpr bool RELAXED = decltype(relaxed)::value, RELAXED_A = decltype(relaxed_a)::value;
+    constexpr bool SKIP_A = decltype(skip_a)::value;  // EARLY, K-step 0: piece 3 of K-tile 1 is out already
     const int slot = kt & 1;
     int ka = kt + 1, kb = kt + 2;
     const int sa = ka >= nk, sb = kb >= nk;
@@ -368,13 +380,14 @@ __device__ __forceinline__ void pingpong2_tiles(bool any, int nk, int grp, Issue
       read(phase_t<2 * SG>{}, slot);
       read(phase_t<2 * SG + 1>{}, slot);
       if constexpr (SG == 0) {
-        issue(sa, ka, slot ^ 1, phase_t<3>{});
+        if constexpr (!SKIP_A) issue(sa, ka, slot ^ 1, phase_t<3>{});
       } else {
         issue(sb, kb, slot, phase_t<0>{});
         issue(sb, kb, slot, phase_t<1>{});
         issue(sb, kb, slot, phase_t<2>{});
       }
-      wait_vmcnt<RELAXED ? 8 + E : 8>();
+      constexpr bool R = RELAXED || (SG == 0 && RELAXED_A);
+      wait_vmcnt<R ? 8 + E : 8>();
       wait_lgkm0();
       pp_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -387,11 +400,51 @@ __device__ __forceinline__ void pingpong2_tiles(bool any, int nk, int grp, Issue
     segment(phase_t<0>{});
     segment(phase_t<1>{});
   };
+  const std::false_type F{};
+  const std::true_type T{};
+  const std::integral_constant<bool, EARLY> EA{};
   for (int ti = 0;; ++ti) {
-    if (ti == 0) kstep(0, std::false_type{});
-    else kstep(0, std::true_type{});
-    for (int kt = 1; kt < nk; ++kt) kstep(kt, std::false_type{});
+    if constexpr (!EARLY) {  // three inlined K-step bodies (more spill)
+      if (ti == 0) kstep(0, F, F, F);
+      else kstep(0, T, F, F);
+      for (int kt = 1; kt < nk; ++kt) kstep(kt, F, F, F);
+    } else {
+      // one K-step body with wave-uniform flags (more inlined bodies spill)
+      for (int kt = 0; kt < nk; ++kt) {
+        const bool r = ti > 0 && kt == 0, ra = ti > 0 && kt == 1, sk = kt == 0;
+        const int slot = kt & 1;
+        int ka = kt + 1, kb = kt + 2;
+        const int sa = ka >= nk, sb = kb >= nk;
+        ka -= sa ? nk : 0;
+        kb -= sb ? nk : 0;
+        auto segment = [&](auto sg) {
+          constexpr int SG = decltype(sg)::value;
+          read(phase_t<2 * SG>{}, slot);
+          read(phase_t<2 * SG + 1>{}, slot);
+          if constexpr (SG == 0) {
+            if (!sk) issue(sa, ka, slot ^ 1, phase_t<3>{});
+          } else {
+            issue(sb, kb, slot, phase_t<0>{});
+            issue(sb, kb, slot, phase_t<1>{});
+            issue(sb, kb, slot, phase_t<2>{});
+          }
+          if (r || (SG == 0 && ra)) wait_vmcnt<8 + E>();
+          else wait_vmcnt<8>();
+          wait_lgkm0();
+          pp_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_setprio(1);
+          mma(phase_t<2 * SG>{});
+          mma(phase_t<2 * SG + 1>{});
+          __builtin_amdgcn_s_setprio(0);
+          pp_barrier();
+        };
+        segment(phase_t<0>{});
+        segment(phase_t<1>{});
+      }
+    }
     if (grp == 0) pp_barrier();  // meet group 1's last barrier: aligned
+    if constexpr (EARLY) issue(1, nk > 1 ? 1 : 0, 1, phase_t<3>{});  // the next tile's K-tile 1, piece 3
     tile_end(ti);
     const bool next = more(ti);
     if (!next) break;
