@@ -53,8 +53,8 @@
 #define SIREN_NT_SEG2 1
 #endif
 
-#ifndef SIREN_NT_EARLY  // measurement: gemm_pipeline.h pingpong2_tiles EARLY
-#define SIREN_NT_EARLY 0
+#ifndef SIREN_NT_EARLY  // gemm_pipeline.h pingpong2_tiles EARLY for every mode (measurement; the fused
+#define SIREN_NT_EARLY 0  // last layer always takes it)
 #endif
 // whole-line epilogue stores as non-temporal (global_store ... nt): cfg4 forward -6.0%, dX -1.3%, cfg2
 // within 0.2% (profiles/r19/ab_full_lines.json u26); 0 = plain stores
@@ -1086,8 +1086,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         for (int j = 0; j < SM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
     if constexpr (SIREN_NT_SEG2 != 0)
-      pingpong2_tiles<epilogue_stores<Cfg, MODE>(), SIREN_NT_EARLY != 0>(in_range(g_cur), nk, wm, issue, read, mma,
-                                                                          set_tiles, tile_end, more);
+      // EARLY (the next tile's K-tile 1 piece 3 before the epilogue's stores): the fused last layer
+      // gains 2.3% (cfg2) / 0.8% (cfg4), the plain forward loses 2.3% at cfg2 (profiles/r20/ab_early.json)
+      pingpong2_tiles<epilogue_stores<Cfg, MODE>(), SIREN_NT_EARLY != 0 || nt_is_hb(MODE)>(
+          in_range(g_cur), nk, wm, issue, read, mma, set_tiles, tile_end, more);
     else
       pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles,
                                                          tile_end, more);
