@@ -119,8 +119,12 @@ struct NtLds {
   static constexpr int QS = IA + (nt_is_snake_fwd(MODE) ? Cfg::VEC : 0);  // dynamic tile queue: 2 tile ids
   // plain forward and dX, ping-pong config: a 2-KiB scratch per wave that turns the epilogue's 16-row x
   // 64-B store pieces into whole 128-B lines (the 128x128 config keeps two blocks per CU without it)
-  static constexpr int ST = QS + 16;
-  static constexpr int SIZE = ST + ((Cfg::PP && (MODE == NT_FWD || MODE == NT_DX) && !HEAD) ? Cfg::NWAVES * 2048 : 0);
+  // (the fused last layer walks statically: no queue slots, and its sine / Tanh kinds fit the scratch
+  // in exactly 160 KiB)
+  static constexpr int ST = QS + (nt_is_hb(MODE) ? 0 : 16);
+  static constexpr bool LINES = Cfg::PP && (((MODE == NT_FWD || MODE == NT_DX) && !HEAD) ||
+                                            MODE == NT_FWD_HB || MODE == NT_FWD_HB_TANH);
+  static constexpr int SIZE = ST + (LINES ? Cfg::NWAVES * 2048 : 0);
   static_assert(SIZE <= 160 * 1024, "LDS");
 };
 
@@ -210,6 +214,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // eighth of the grid in order, so the blocks holding one row band are the ones that started
   // it at the same time.
   constexpr bool dyn = Cfg::PP && QUEUE;
+  static_assert(!(dyn && nt_is_hb(MODE)), "the fused last layer walks statically (no queue slots in LDS)");
   // global tile id g -> origin; the static walk's i-th tile of this block is g = bp + i * G
   auto tile_of = [&](int g, int& m0, int& n0) {
     const int tm = tn_pow2 ? (g >> tn_shift) : g / tiles_n;
@@ -280,6 +285,30 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     if constexpr (SIREN_NT_STNT != 0) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (u32x4*)dst);
     else *(uint4*)dst = v;
+  };
+  // Whole 128-B lines per store (Lay::LINES): the wave's 16-row x 64-column fp16 piece of one
+  // output (lane: row lane & 15, 16-B chunks 4 pp + swap16_col(lane) / 8) goes through its 2-KiB LDS
+  // scratch, 16-B chunks XOR-swizzled by row (conflict-free both ways), and each store writes rows
+  // 8q .. 8q+7 as 8 lanes x 16 B per row.  Same bytes and store count as 16 rows x 64 B, but no
+  // half-line writes.  Same-wave LDS accesses complete in order, so the reads see this
+  // wave's writes and the next output's writes follow the reads.  row = this lane's row, col = the
+  // wave's first column.
+  auto lines_out = [&](h16* out, int row, int col, const uint4 (&v)[Cfg::SN / 2]) {
+    static_assert(Cfg::SN == 4, "a wave's row piece is one 128-B line");
+    char* sc = smem + Lay::ST + wave * 2048;
+    const int pr = lane & 15, pc = swap16_col(lane) >> 3;  // this lane's piece: row, 16-B chunk
+    const int qr = lane >> 3, qc = lane & 7;                // line layout: row (+ 8 q), chunk
+#pragma unroll
+    for (int pp = 0; pp < Cfg::SN / 2; ++pp) {
+      const int c = pp * 4 + pc;
+      *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = v[pp];
+    }
+    const size_t fbase = (size_t)(row - pr + qr) * N + col + qc * 8;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = qr + 8 * q;
+      stl(out + fbase + (size_t)(8 * q) * N, *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4)));
+    }
   };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
@@ -546,6 +575,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int pp = 0; pp < SN / 2; ++pp)
             eall[j][pp] = *(const uint4*)(p.E + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
         }
+        uint4 dzq[SN / 2];  // whole-line stores (Lay::LINES): this row piece's two 16-B pieces
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
           uint2 dzp[2];
@@ -572,8 +602,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             });
             dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
           }
-          st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+          if constexpr (Lay::LINES) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
+          else st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
         }
+        if constexpr (Lay::LINES) lines_out(p.dZ, mrow0 + j * 16, n0 + wn * TN, dzq);
       }
 #pragma unroll
       for (int pp = 0; pp < SN / 2; ++pp)
@@ -711,32 +743,11 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           asm volatile("" ::"v"(keep));
           continue;
         }
-        if constexpr (Cfg::PP && MODE == NT_FWD && !HEAD) {
-          // Whole 128-B lines per store: the wave's 16-row x 64-column piece of Y (then of C) goes
-          // through its 2-KiB LDS scratch (16-B chunks XOR-swizzled by row: conflict-free both ways),
-          // and each store writes rows 8q .. 8q+7 as 8 lanes x 16 B per row.  Same bytes and store
-          // count as 16 rows x 64 B, but no half-line writes: forward -4.6%, cfg4 -6.5% (static walk,
-          // profiles/r19/ab_full_lines.json).  Same-wave LDS accesses complete in order, so the reads
-          // see this wave's writes and the next output's writes follow the reads.
-          char* sc = smem + Lay::ST + wave * 2048;
-          const int pr = lane & 15, pc = swap16_col(lane) >> 3;  // this lane's piece: row, 16-B chunk
-          const int qr = lane >> 3, qc = lane & 7;                // line layout: row (+ 8 q), chunk
-          const size_t fbase = (size_t)(mrow0 - pr + j * 16 + qr) * N + (n0 + wn * TN) + qc * 8;
-          auto lines = [&](h16* out, const uint4 (&v)[SN / 2]) {
-#pragma unroll
-            for (int pp = 0; pp < SN / 2; ++pp) {
-              const int c = pp * 4 + pc;
-              *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = v[pp];
-            }
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const int r = qr + 8 * q;
-              stl(out + fbase + (size_t)(8 * q) * N, *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4)));
-            }
-          };
-          static_assert(SN == 4, "a wave's row piece is one 128-B line");
-          lines(p.Y, yp);
-          lines(p.C, cpk);
+        if constexpr (Lay::LINES && MODE == NT_FWD) {
+          // whole-line stores (lines_out): forward -4.6%, cfg4 -6.5% (static walk,
+          // profiles/r19/ab_full_lines.json)
+          lines_out(p.Y, mrow0 + j * 16, n0 + wn * TN, yp);
+          lines_out(p.C, mrow0 + j * 16, n0 + wn * TN, cpk);
           continue;
         }
 #pragma unroll
@@ -906,26 +917,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               });
               dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
             }
-            if constexpr (MODE == NT_DX && Cfg::PP) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
+            if constexpr (Lay::LINES && MODE == NT_DX) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
             else if constexpr (MODE == NT_DX) st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
           }
-          if constexpr (MODE == NT_DX && Cfg::PP) {
-            // whole 128-B dZ lines per store through the wave's LDS scratch (as the forward's Y / C)
-            char* sc = smem + Lay::ST + wave * 2048;
-            const int pr = lane & 15, pc = swap16_col(lane) >> 3;
-            const int qr = lane >> 3, qc = lane & 7;
-#pragma unroll
-            for (int pp = 0; pp < SN / 2; ++pp) {
-              const int c = pp * 4 + pc;
-              *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = dzq[pp];
-            }
-            const size_t fbase = (size_t)(mrow0 - pr + j * 16 + qr) * N + (n0 + wn * TN) + qc * 8;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const int r = qr + 8 * q;
-              stl(p.dZ + fbase + (size_t)(8 * q) * N, *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4)));
-            }
-          }
+          if constexpr (Lay::LINES && MODE == NT_DX) lines_out(p.dZ, mrow0 + j * 16, n0 + wn * TN, dzq);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {

@@ -16,7 +16,8 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "inr-for-audio_amd", "csrc")
-SOURCES = ["capi.hip", "gemm_nt.hip", "gemm_tn.hip", "elementwise.hip", "kan.hip", "layer_fp32.hip"]
+sys.path.insert(0, os.path.join(ROOT, "inr-for-audio_amd"))
+from buildinfo import SOURCES  # noqa: E402  (the product library's source list)
 
 _ST16 = "  auto st16 = [&](h16* dst, uint4 v) { *(uint4*)dst = v; };"
 
@@ -319,6 +320,11 @@ _DXS_NT_NEW2 = """                cq[jj] = ldnt(p.Cprev + off);
                 eq[jj] = ldnt(p.Eprev + off);"""
 VARIANTS["dxs_nt"] = {"gemm_nt.hip": [(_DXS_NT_HELPER_OLD, _DXS_NT_HELPER_NEW), (_DXS_NT_OLD1, _DXS_NT_NEW1),
                                       (_DXS_NT_OLD2, _DXS_NT_NEW2)]}
+
+# the fused last layer with the plain 16-row x 64-B dZ_L stores (before the whole-line scratch)
+VARIANTS["hbplain"] = {"gemm_nt.hip": [("""                                            MODE == NT_FWD_HB || MODE == NT_FWD_HB_TANH);""",
+                                        """                                            false);""")]}
+
 
 
 def build(name: str, extra_defines=()) -> str:
