@@ -28,6 +28,9 @@ extern "C" {
 
 #define SIREN_ABI_VERSION 12
 #define SIREN_MAX_INNER 16  /* max hidden layers (num_sine + num_snake + num_tanh) */
+/* hidden widths: 128, 256, 512, 1024, then multiples of 1024 up to this (run as 1024-column
+ * windows; models.py pads any other width to the next of these) */
+#define SIREN_MAX_HIDDEN 4096
 #define SIREN_ROW_TILE 128  /* coordinate rows are padded to a multiple of this */
 /* ints in one tile-queue counter set (siren_batch.tileq, siren_inner_fwd's tileq): the
  * hidden-layer forward GEMM's persistent blocks pull their tiles from it.  Caller-owned device

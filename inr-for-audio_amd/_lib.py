@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsiren_hip.so")
 ABI_VERSION = 12
 MAX_INNER = 16
+MAX_HIDDEN = 4096  # SIREN_MAX_HIDDEN: hidden widths 128, 256, 512, 1024, then multiples of 1024 up to this
 ROW_TILE = 128
 TILEQ_INTS = 768  # SIREN_TILEQ_INTS: one tile-queue counter set
 ACT_SINE, ACT_SNAKE, ACT_TANH = 0, 1, 2  # siren_act

@@ -61,7 +61,11 @@ inline void prof_end(hipStream_t s, int launches = 1) {
     if (_pe != hipSuccess) return _pe;       \
   } while (0)
 
-bool hidden_ok(int h) { return h >= 128 && h % 128 == 0 && h <= 1024 && 256 % (h / 4) == 0; }
+// 128, 256, 512, 1024 (one launch per GEMM), then multiples of 1024 up to SIREN_MAX_HIDDEN (column
+// windows of 1024: gemm_nt, first_fwd, head_bwd)
+bool hidden_ok(int h) {
+  return (h >= 128 && h % 128 == 0 && h <= 1024 && 256 % (h / 4) == 0) || (h > 1024 && h % 1024 == 0 && h <= SIREN_MAX_HIDDEN);
+}
 
 int check_net(const siren_net* n) {
   if (!n) return SIREN_ERR_NULL;
@@ -474,7 +478,8 @@ int siren_first_fwd(const float* t, int32_t in_dim, const float* W0, const float
                     int32_t rows, int32_t hidden, uint16_t* Y0, uint16_t* C0, void* stream) {
   if (!t || !W0 || !b0 || !Y0 || !C0) return SIREN_ERR_NULL;
   if (in_dim < 1 || in_dim > 2) return SIREN_ERR_CONFIG;
-  if (rows < 0 || hidden < 8 || hidden > 2048 || hidden % 8 || 256 % (hidden / 8)) return SIREN_ERR_SHAPE;
+  if (rows < 0 || hidden < 8 || hidden % 8 || (hidden <= 2048 ? 256 % (hidden / 8) != 0 : (hidden % 1024 || hidden > SIREN_MAX_HIDDEN)))
+    return SIREN_ERR_SHAPE;
   return (int)first_fwd(t, in_dim, W0, b0, omega0, rows, hidden, B(Y0), B(C0), S(stream));
 }
 

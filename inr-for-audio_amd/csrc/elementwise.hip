@@ -90,7 +90,7 @@ template <bool STORE_C, bool SNAKE>
 __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const float* __restrict__ W0,
                                  const float* __restrict__ b0, float omega0, int R, int H,
                                  h16* __restrict__ Y0, h16* __restrict__ C0, const float* __restrict__ a0,
-                                 h16* __restrict__ E0) {
+                                 h16* __restrict__ E0, int ld) {
   const int tpr = H >> 3;
   const int rpb = blockDim.x / tpr;
   const int lt = threadIdx.x % tpr, lr = threadIdx.x / tpr;
@@ -133,34 +133,43 @@ __global__ void first_fwd_kernel(const float* __restrict__ t, int in_dim, const 
       yv[r] = (h16)y[r];
       cv[r] = (h16)c[r];
     }
-    *(h16x8*)(Y0 + m * H + n) = yv;
-    if constexpr (STORE_C) *(h16x8*)(C0 + m * H + n) = cv;
+    *(h16x8*)(Y0 + m * ld + n) = yv;
+    if constexpr (STORE_C) *(h16x8*)(C0 + m * ld + n) = cv;
     if constexpr (SNAKE) {
       h16x8 evv;
 #pragma unroll
       for (int r = 0; r < 8; ++r) evv[r] = (h16)ev[r];
-      *(h16x8*)(E0 + m * H + n) = evv;
+      *(h16x8*)(E0 + m * ld + n) = evv;
     }
   }
 }
 
 hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b0, float omega0,
                      int R, int H, h16* Y0, h16* C0, hipStream_t s, const float* a0, h16* E0) {
-  if (H % 8 || H > 2048 || 256 % (H / 8) || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
+  // widths above 2048 run as launches over 1024-column windows (row stride H; every element's
+  // arithmetic is its own column's, so the result is the one-launch result)
+  const int win = H <= 2048 ? H : 1024;
+  if (H % 8 || 256 % (win / 8) || H % win || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
   if ((a0 != nullptr) != (E0 != nullptr) || (a0 && !C0)) return hipErrorInvalidValue;
-  const int rpb = 256 / (H / 8);
+  const int rpb = 256 / (win / 8);
   const dim3 grid(grid_for(R, rpb, 4096));
-  // C0 == NULL: Y0 only (the cos is not needed); a0 != NULL: Linear + Snake first layer
-  if (a0)
-    hipLaunchKernelGGL((first_fwd_kernel<true, true>), grid, dim3(256), 0, s, t, in_dim, W0, b0, omega0, R, H, Y0,
-                       C0, a0, E0);
-  else if (C0)
-    hipLaunchKernelGGL((first_fwd_kernel<true, false>), grid, dim3(256), 0, s, t, in_dim, W0, b0, omega0, R, H, Y0,
-                       C0, a0, E0);
-  else
-    hipLaunchKernelGGL((first_fwd_kernel<false, false>), grid, dim3(256), 0, s, t, in_dim, W0, b0, omega0, R, H, Y0,
-                       C0, a0, E0);
-  return hipGetLastError();
+  auto off = [](auto* v, int nb) { return v ? v + nb : v; };
+  for (int nb = 0; nb < H; nb += win) {
+    const float* W0w = W0 + (size_t)nb * in_dim;
+    // C0 == NULL: Y0 only (the cos is not needed); a0 != NULL: Linear + Snake first layer
+    if (a0)
+      hipLaunchKernelGGL((first_fwd_kernel<true, true>), grid, dim3(256), 0, s, t, in_dim, W0w, b0 + nb, omega0, R,
+                         win, Y0 + nb, off(C0, nb), a0 + nb, off(E0, nb), H);
+    else if (C0)
+      hipLaunchKernelGGL((first_fwd_kernel<true, false>), grid, dim3(256), 0, s, t, in_dim, W0w, b0 + nb, omega0, R,
+                         win, Y0 + nb, C0 + nb, a0, E0, H);
+    else
+      hipLaunchKernelGGL((first_fwd_kernel<false, false>), grid, dim3(256), 0, s, t, in_dim, W0w, b0 + nb, omega0, R,
+                         win, Y0 + nb, C0, a0, E0, H);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // ---------------------------------------------------------------------------------
@@ -348,7 +357,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     const h16* __restrict__ C, const h16* __restrict__ Y, const float* __restrict__ g,
     const float* __restrict__ w_head, float omega, int R, int H, const float* __restrict__ gscale,
     h16* __restrict__ dZ, float* __restrict__ db_part, float* __restrict__ dwh_part,
-    const h16* __restrict__ E, float* __restrict__ da_part) {
+    const h16* __restrict__ E, float* __restrict__ da_part, int ld) {
   typedef _Float16 hv __attribute__((ext_vector_type(V)));
   __shared__ float red[3][256 * V];
   const float S = gscale ? gscale[0] : 1.0f;  // dZ storage scale (grad_scale)
@@ -367,10 +376,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   for (int r = rg; r < 128; r += nrg) {
     const int64_t m = m0 + r;
     const float gm = g[m];
-    const hv c = *(const hv*)(C + m * H + n);
-    const hv yv = *(const hv*)(Y + m * H + n);
+    const hv c = *(const hv*)(C + m * ld + n);
+    const hv yv = *(const hv*)(Y + m * ld + n);
     hv ev = {};
-    if (E) ev = *(const hv*)(E + m * H + n);
+    if (E) ev = *(const hv*)(E + m * ld + n);
     hv out;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
@@ -380,7 +389,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       da[k] += (gm * wv[k]) * (float)ev[k];
       out[k] = (_Float16)(dz * S);
     }
-    *(hv*)(dZ + m * H + n) = out;
+    *(hv*)(dZ + m * ld + n) = out;
   }
 #pragma unroll
   for (int k = 0; k < V; ++k) {
@@ -397,23 +406,33 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       b += red[1][(gi * hq + q) * V + k];
       d += red[2][(gi * hq + q) * V + k];
     }
-    db_part[(size_t)blockIdx.x * H + c] = a;
-    dwh_part[(size_t)blockIdx.x * H + c] = b;
-    if (E) da_part[(size_t)blockIdx.x * H + c] = d;
+    db_part[(size_t)blockIdx.x * ld + c] = a;
+    dwh_part[(size_t)blockIdx.x * ld + c] = b;
+    if (E) da_part[(size_t)blockIdx.x * ld + c] = d;
   }
 }
 
 hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_head, float omega,
                     int R, int H, const float* gscale, h16* dZ, float* db_part, float* dwh_part,
                     const h16* E, float* da_part, hipStream_t s) {
-  if (R % 128 || H % 4 || 256 % (H / 4) || (E && !da_part)) return hipErrorInvalidValue;
-  if (H % 8 == 0 && 256 % (H / 8) == 0)
-    hipLaunchKernelGGL(head_bwd_kernel<8>, dim3(R / 128), dim3(256), 0, s, C, Y, g, w_head, omega, R, H,
-                       gscale, dZ, db_part, dwh_part, E, da_part);
-  else
-    hipLaunchKernelGGL(head_bwd_kernel<4>, dim3(R / 128), dim3(256), 0, s, C, Y, g, w_head, omega, R, H,
-                       gscale, dZ, db_part, dwh_part, E, da_part);
-  return hipGetLastError();
+  // widths above 2048: launches over 1024-column windows (row stride H), each column's sums as in one
+  const int win = H <= 2048 ? H : 1024;
+  if (R % 128 || win % 4 || H % win || (E && !da_part)) return hipErrorInvalidValue;
+  const bool v8 = win % 8 == 0 && 256 % (win / 8) == 0;
+  if (!v8 && 256 % (win / 4)) return hipErrorInvalidValue;
+  for (int nb = 0; nb < H; nb += win) {
+    const h16* Ew = E ? E + nb : E;
+    float* daw = da_part ? da_part + nb : da_part;
+    if (v8)
+      hipLaunchKernelGGL(head_bwd_kernel<8>, dim3(R / 128), dim3(256), 0, s, C + nb, Y + nb, g, w_head + nb, omega, R,
+                         win, gscale, dZ + nb, db_part + nb, dwh_part + nb, Ew, daw, H);
+    else
+      hipLaunchKernelGGL(head_bwd_kernel<4>, dim3(R / 128), dim3(256), 0, s, C + nb, Y + nb, g, w_head + nb, omega, R,
+                         win, gscale, dZ + nb, db_part + nb, dwh_part + nb, Ew, daw, H);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // ---------------------------------------------------------------------------------

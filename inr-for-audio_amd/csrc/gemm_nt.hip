@@ -193,7 +193,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
-  const int K = p.K, N = p.N;
+  // N: this launch's columns (a window of at most MAXN of a wider layer: gemm_nt); LD: the row stride
+  // of every [M][*] operand and output (the layer's full width; the host offsets the pointers)
+  const int K = p.K, N = p.N, LD = p.ld;
   const int tiles_n = N / BN;
   const int ntiles = (p.M / BM) * tiles_n;
   const bool tn_pow2 = (tiles_n & (tiles_n - 1)) == 0;  // N / BN is 1, 2, 4 or 8 at H <= 1024
@@ -303,11 +305,11 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       const int c = pp * 4 + pc;
       *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = v[pp];
     }
-    const size_t fbase = (size_t)(row - pr + qr) * N + col + qc * 8;
+    const size_t fbase = (size_t)(row - pr + qr) * LD + col + qc * 8;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int r = qr + 8 * q;
-      stl(out + fbase + (size_t)(8 * q) * N, *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4)));
+      stl(out + fbase + (size_t)(8 * q) * LD, *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4)));
     }
   };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
@@ -360,11 +362,11 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       for (int j = 0; j < PRE_J; ++j)
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp)
-          cp_in[j][pp] = *(const uint4*)(p.Cprev + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
+          cp_in[j][pp] = *(const uint4*)(p.Cprev + (size_t)(mrow0 + j * 16) * LD + npc + pp * 32);
       if constexpr (HAS_E) {
 #pragma unroll
         for (int j = 0; j < EB; ++j) {
-          const size_t off = (size_t)(mrow0 + j * 16) * N + npc;
+          const size_t off = (size_t)(mrow0 + j * 16) * LD + npc;
           ce_in[j][0] = *(const uint4*)(p.Cprev + off);
           ce_in[j][1] = *(const uint4*)(p.Eprev + off);
         }
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             }
             hp[j] += sv[0] * hw[i].x + sv[1] * hw[i].y + sv[2] * hw[i].z + sv[3] * hw[i].w;
           }
-          if constexpr (SNK) st16(p.E + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(epair[0], epair[1]));
+          if constexpr (SNK) st16(p.E + (size_t)(mrow0 + j * 16) * LD + npc + pp * 32, swap16_pair(epair[0], epair[1]));
         }
       }
 #pragma unroll
@@ -573,7 +575,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         if constexpr (SNK) {
 #pragma unroll
           for (int pp = 0; pp < SN / 2; ++pp)
-            eall[j][pp] = *(const uint4*)(p.E + (size_t)(mrow0 + j * 16) * N + npc + pp * 32);
+            eall[j][pp] = *(const uint4*)(p.E + (size_t)(mrow0 + j * 16) * LD + npc + pp * 32);
         }
         uint4 dzq[SN / 2];  // whole-line stores (Lay::LINES): this row piece's two 16-B pieces
 #pragma unroll
@@ -603,7 +605,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
           }
           if constexpr (Lay::LINES) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
-          else st16(p.dZ + (size_t)(mrow0 + j * 16) * N + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+          else st16(p.dZ + (size_t)(mrow0 + j * 16) * LD + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
         }
         if constexpr (Lay::LINES) lines_out(p.dZ, mrow0 + j * 16, n0 + wn * TN, dzq);
       }
@@ -668,7 +670,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           float sum = 0.f;
 #pragma unroll
           for (int w = 0; w < Cfg::WM; ++w) sum += red[(q * Cfg::WM + w) * BN + tid];
-          p.colsum_part[((size_t)tm * NP + q) * N + n0 + tid] = sum * invS;  // sums of x S: exact
+          p.colsum_part[((size_t)tm * NP + q) * LD + n0 + tid] = sum * invS;  // sums of x S: exact
         }
       }
     } else if constexpr (nt_is_fwd(MODE)) {
@@ -686,7 +688,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       for (int j = 0; j < SM; ++j) hp[j] = 0.f;
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
-        const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
+        const size_t rowoff = (size_t)(mrow0 + j * 16) * LD;
         uint4 yp[SN / 2], cpk[SN / 2], epk[SN / 2];
 #pragma unroll
         for (int q = 0; q < SN / 2; ++q) {
@@ -814,7 +816,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       // partial sums its rows in order 0 .. SM-1 whatever order the pieces go in
       auto piece = [&](auto jc, auto ppc, const uint4& cpv, const uint4& epv) {
         constexpr int j = decltype(jc)::value, pp = decltype(ppc)::value;
-        const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
+        const size_t rowoff = (size_t)(mrow0 + j * 16) * LD;
         float t0 = 0.f, t1 = 0.f;
         if constexpr (nt_is_dx0(MODE)) {
           t0 = t_in[j][0];
@@ -864,7 +866,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                 cq[bf][jj][pp] = ce_in[jj][0];
                 eq[bf][jj][pp] = ce_in[jj][1];
               } else {
-                const size_t off = (size_t)(mrow0 + (bq * EB + jj) * 16) * N + npc + pp * 32;
+                const size_t off = (size_t)(mrow0 + (bq * EB + jj) * 16) * LD + npc + pp * 32;
                 cq[bf][jj][pp] = *(const uint4*)(p.Cprev + off);
                 eq[bf][jj][pp] = *(const uint4*)(p.Eprev + off);
               }
@@ -887,7 +889,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         // written through the lambda, NT_DX0 takes 252-256 VGPRs instead of 239-244 (gfx950 listing)
 #pragma unroll
         for (int j = 0; j < SM; ++j) {
-          const size_t rowoff = (size_t)(mrow0 + j * 16) * N;
+          const size_t rowoff = (size_t)(mrow0 + j * 16) * LD;
           float t0 = 0.f, t1 = 0.f;
           if constexpr (nt_is_dx0(MODE)) {
             t0 = t_in[j][0];
@@ -943,7 +945,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           float s = 0.f;
 #pragma unroll
           for (int w = 0; w < Cfg::WM; ++w) s += red[(q * Cfg::WM + w) * BN + tid];
-          p.colsum_part[((size_t)tm * nred + q) * N + n0 + tid] = s * inv_scale;
+          p.colsum_part[((size_t)tm * nred + q) * LD + n0 + tid] = s * inv_scale;
         }
       }
     }
@@ -1256,7 +1258,7 @@ bool gemm_nt_head_fusable(int M, int N, hipStream_t s, int mode) {
   return hb_coresident(mode, ntiles < cap ? ntiles : cap, s);
 }
 
-hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
+static hipError_t gemm_nt_window(int mode, bool head, const NtParams& p, hipStream_t s) {
   if (p.M % NtSmall::BM || p.N % NtSmall::BN || p.K % NtSmall::BK || p.M <= 0 || p.N > NtSmall::MAXN) return hipErrorInvalidValue;
   if (nt_is_hb(mode)) {
     if (!head || p.tile != 256 || !gemm_nt_head_fusable(p.M, p.N, s, mode)) return hipErrorInvalidValue;
@@ -1291,10 +1293,10 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
     if (p.M % 256 || p.N % 256) return hipErrorInvalidValue;
     const int pipe = g_nt_pipe >= 0 ? g_nt_pipe : 4;
     // pipe 5: the forward with its epilogue under the next tile's MFMAs (gemm_nt1.hip)
-    if ((pipe == 5 || pipe == 7) && mode == NT_FWD && !head && gemm_nt_one_ok(p))
+    if ((pipe == 5 || pipe == 7) && mode == NT_FWD && !head && p.ld == p.N && gemm_nt_one_ok(p))
       return gemm_nt_one(p, g_nt_grid_cap > 0 ? g_nt_grid_cap : stream_cus(s), g_nt_diag, pipe == 5, s);
     // pipe 6: the forward with one wave per SIMD on 256x256 tiles (gemm_nt2.hip)
-    if (pipe == 6 && mode == NT_FWD && !head && gemm_nt_big_ok(p))
+    if (pipe == 6 && mode == NT_FWD && !head && p.ld == p.N && gemm_nt_big_ok(p))
       return gemm_nt_big(p, g_nt_grid_cap > 0 ? g_nt_grid_cap : stream_cus(s), g_nt_diag, s);
     switch (pipe) {
       case 0: return dispatch_mode<NtLarge>(mode, head, p, s, false);
@@ -1307,6 +1309,41 @@ hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
   }
   if (p.tile != 128) return hipErrorInvalidValue;
   return dispatch_mode<NtSmall>(mode, head, p, s, false);
+}
+
+// A layer wider than the epilogue's per-column LDS vectors (MAXN = 1024 columns) runs as launches over
+// column windows of MAXN: each window is the same GEMM on rows nb .. nb + MAXN of W with its slice
+// of every per-column vector, its column slice of every [M][N] operand (row stride p.N, NtParams::ld)
+// and its tiles' head partials.  Every output element and column partial is computed exactly as in
+// one launch over all N (a column's arithmetic never involves another column), so the windowed
+// result is the one-launch result.  The fused last layer (one band's column tiles hand off their
+// head partials) is not windowed: gemm_nt_head_fusable is false above 4 column tiles.
+hipError_t gemm_nt(int mode, bool head, const NtParams& p, hipStream_t s) {
+  constexpr int WIN = NtSmall::MAXN;
+  static_assert(NtSmall::MAXN == NtLargePP::MAXN && NtSmall::MAXN == NtLarge::MAXN, "one window width");
+  NtParams q = p;
+  q.ld = p.N;
+  if (p.N <= WIN || nt_is_hb(mode)) return gemm_nt_window(mode, head, q, s);
+  if (p.N % WIN || p.tile <= 0 || p.tile > 256) return hipErrorInvalidValue;
+  for (int nb = 0; nb < p.N; nb += WIN) {
+    q.N = WIN;
+    q.W = p.W + (size_t)nb * p.K;
+    auto col = [&](auto* v) { return v ? v + nb : v; };
+    q.bias = col(p.bias);
+    q.act_a = col(p.act_a);
+    q.head_w = col(p.head_w);
+    q.Y = col(p.Y);
+    q.C = col(p.C);
+    q.E = col(p.E);
+    q.Cprev = col(p.Cprev);
+    q.Eprev = col(p.Eprev);
+    q.dZ = col(p.dZ);
+    q.colsum_part = col(p.colsum_part);
+    q.head_part = p.head_part ? p.head_part + (size_t)(nb / p.tile) * p.M : nullptr;
+    const hipError_t e = gemm_nt_window(mode, head, q, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace siren

@@ -27,6 +27,8 @@ struct NtParams {
   const h16* X;  // [M][K]
   const h16* W;  // [N][K]
   int M, N, K;
+  int ld;         // row stride of the [M][*] operands and outputs: gemm_nt sets it (= N; column
+                  // windows of a layer wider than 1024 keep the layer's width)
   int tile;       // 128 or 256 (nt_choose_tile): partials are per tile-row / tile-column
   float omega;  // FWD: this layer's omega; DX: omega of the layer below; DX0: omega_0
   // NT_FWD

@@ -145,16 +145,19 @@ class SirenWithSnakeTanh(nn.Module):
                        0.0 if self.last_linear else float(self.hidden_omega_0))
 
     def hip_width(self) -> int:
-        """The hidden width the kernels run at: hidden_features itself when it is 128, 256, 512
-        or 1024, else the next of those -- the network is zero-padded to it (hip_padding), which
-        computes the unpadded network's function and gradients exactly (padded units have zero
-        weights in and out: their outputs are 0 and every gradient that touches them is 0)."""
+        """The hidden width the kernels run at: hidden_features itself when it is 128, 256, 512,
+        1024 or a multiple of 1024 up to SIREN_MAX_HIDDEN (4096: the GEMM epilogues and the
+        elementwise kernels run 1024-column windows of it), else the next of those -- the network is
+        zero-padded to it (hip_padding), which computes the unpadded network's function and
+        gradients exactly (padded units have zero weights in and out: their outputs are 0 and every
+        gradient that touches them is 0).  The reference takes any width (models.py:310-311)."""
         H = int(self.hidden_features)
         for w in (128, 256, 512, 1024):
             if H <= w:
                 return w
-        raise NotImplementedError(f"HIP path: hidden_features <= 1024 (the NT epilogue's per-column LDS "
-                                  f"vectors), got {H}")
+        if H <= _lib.MAX_HIDDEN:
+            return -(-H // 1024) * 1024
+        raise NotImplementedError(f"HIP path: hidden_features <= {_lib.MAX_HIDDEN} (SIREN_MAX_HIDDEN), got {H}")
 
     def hip_padding(self) -> dict:
         """{parameter index: (stored shape, fill)} for engine.ParamLayout when hidden_features is

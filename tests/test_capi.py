@@ -106,6 +106,14 @@ def test_supported_hidden_sizes_validate(lib, hidden):
                               None, None, None, None) == 1002
 
 
+@pytest.mark.parametrize("hidden,ok", [(128, True), (1024, True), (2048, True), (3072, True), (4096, True),
+                                       (384, False), (1536, False), (5120, False)])
+def test_hidden_width_shapes(lib, hidden, ok):
+    """Kernel widths: 128, 256, 512, 1024, then multiples of 1024 up to SIREN_MAX_HIDDEN (column windows);
+    a width outside them is a shape error before any other check (here the bad tile 64: 1003)."""
+    assert lib.siren_inner_bwd_dw(1, 1, 128, hidden, 1, 64, 1, None) == (1003 if ok else 1001)
+
+
 def test_set_option_ranges(lib):
     """siren_set_option validates every knob on the host (SIREN_OPT_* in siren_hip.h) and leaves
     the defaults restored; SIREN_OPT_NT_QUEUE takes 0 (static walk), 1 (forward modes), 2 (all).

@@ -218,6 +218,8 @@ def test_tiny_and_ragged_inputs(dev, n):
     (100, (2, 0, 0), 1500, False, True),     # a width the reference accepts (models.py:310), padded to 128
     (200, (1, 1, 0), 1500, True, False),     # Linear + Snake first, Snake a padded with 1, final SineLayer
     (384, (1, 0, 1), 1024, False, True),     # padded to 512, Tanh last
+    (1500, (2, 0, 0), 1024, False, True),    # padded to 2048: two 1024-column windows per GEMM, unfused head
+    (2100, (1, 1, 1), 512, False, True),     # padded to 3072 (three windows), sine + Snake + Tanh last
 ])
 def test_padded_hidden_width_vs_oracle(dev, H, cfg, n, fl, ll):
     """hidden_features that is not 128/256/512/1024 runs zero-padded to the next kernel width: the
@@ -279,3 +281,32 @@ def test_padded_width_autograd_dropin(dev):
     ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(ref_out, y.numpy()), 1000.0, 30.0, half=True)
     got = {k: v.grad.detach().cpu().numpy() for k, v in model.named_parameters()}
     check_grads("padded_width_autograd", got, ref)
+
+
+@pytest.mark.parametrize("H,n", [(2048, 16384), (4096, 2048)])
+def test_wide_hidden_windows_vs_oracle(dev, H, n):
+    """Hidden widths above 1024 (the reference takes any, models.py:310-311) run every GEMM, the
+    first layer and the head backward over 1024-column windows (gemm_nt, first_fwd, head_bwd):
+    one step's gradients equal the oracle's.  16384 rows x 2048 takes the 256x256 ping-pong tiles
+    (512 tiles), 2048 rows x 4096 the 128x128 ones."""
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(5)
+    model = SirenWithSnakeTanh(1, 1, H, 2, 0, 0, first_linear=False, last_linear=True, first_omega_0=1000.0,
+                               hidden_omega_0=30.0)
+    sd0 = _sd(model)
+    t, y = _signal(n)
+    eng = SirenEngine(model, t, y, lr=1e-3, device=dev)
+    assert eng.spec.hidden == H
+    with torch.no_grad():  # inference at the initial weights (the step below updates them)
+        a = eng.infer(t.to(dev)).cpu().numpy().reshape(-1)
+    eng.step()
+    torch.cuda.synchronize()
+    got = {k: v.detach().cpu().numpy() for k, v in zip(eng.layout.names, eng.grad_views())}
+    p = orc.Params.from_state_dict(sd0, 2, 0, 0, False, True)
+    out, cache = orc.forward(p, t.numpy(), 1000.0, 30.0, half=True, dtype=np.float64)
+    ref = orc.backward(p, t.numpy(), cache, orc.mse_grad(out, y.numpy()), 1000.0, 30.0, half=True)
+    check_grads(f"wide_hidden_step[{H}x{n}]", got, ref)
+    err = float(np.max(np.abs(a - out.reshape(-1))))
+    log(f"wide_hidden_infer[{H}x{n}]", err=err, scale=float(np.max(np.abs(out))))
+    assert err <= 1e-3 * float(np.max(np.abs(out))) + 1e-5

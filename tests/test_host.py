@@ -56,9 +56,11 @@ def test_param_layout():
 
 @pytest.mark.parametrize("H,cfg,fl,ll,Hp", [
     (100, (2, 0, 0), False, True, 128), (384, (1, 1, 1), False, True, 512), (200, (0, 2, 0), True, False, 256),
-    (1000, (1, 0, 0), False, True, 1024), (3, (1, 1, 0), False, True, 128)])
+    (1000, (1, 0, 0), False, True, 1024), (3, (1, 1, 0), False, True, 128),
+    (1500, (2, 0, 0), False, True, 2048), (2048, (1, 0, 1), False, True, 2048), (3000, (1, 1, 1), True, False, 3072)])
 def test_hidden_width_padding(H, cfg, fl, ll, Hp):
-    """Any hidden_features <= 1024 runs zero-padded to the next kernel width (models.py:310 accepts
+    """Any hidden_features <= 4096 runs zero-padded to the next kernel width (128, 256, 512, 1024,
+    then multiples of 1024; models.py:310 accepts
     any width): the layout stores the padded tensors, the model's parameters are their [:H] blocks,
     a Snake a's pad entries are 1 and every other pad entry is 0."""
     from inr_for_audio_amd.engine import ParamLayout
@@ -90,7 +92,7 @@ def test_hip_spec_validation():
     from inr_for_audio_amd.models import SirenWithSnakeTanh
     spec = _model(256, 2, 22000.0).hip_spec()
     assert (spec.in_dim, spec.hidden, spec.n_inner, spec.omega0, spec.omega) == (1, 256, 2, 22000.0, 30.0)
-    bad = [dict(hidden_features=1100), dict(num_sine=0), dict(in_features=3), dict(out_features=2),
+    bad = [dict(hidden_features=4097), dict(num_sine=0), dict(in_features=3), dict(out_features=2),
            dict(num_sine=10, num_snake=4, num_tanh=3)]
     for kw in bad:
         args = dict(in_features=1, out_features=1, hidden_features=256, num_sine=2, num_snake=0, num_tanh=0)

@@ -326,6 +326,10 @@ VARIANTS["hbplain"] = {"gemm_nt.hip": [("""                                     
                                         """                                            false);""")]}
 
 
+# the EARLY tile-boundary schedule (gemm_pipeline.h pingpong2_tiles) for dX and dX0 too
+VARIANTS["early_dx"] = {"gemm_nt.hip": [("SIREN_NT_EARLY != 0 || nt_is_hb(MODE)>(",
+                                         "SIREN_NT_EARLY != 0 || nt_is_hb(MODE) || MODE == NT_DX || MODE == NT_DX0>(")]}
+
 
 def build(name: str, extra_defines=()) -> str:
     patches = VARIANTS[name]
