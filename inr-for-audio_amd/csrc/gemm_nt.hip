@@ -54,8 +54,8 @@
 #endif
 
 #ifndef SIREN_NT_EARLY  // gemm_pipeline.h pingpong2_tiles EARLY for every mode (measurement; the fused
-#define SIREN_NT_EARLY 0  // last layer always takes it)
-#endif
+#define SIREN_NT_EARLY 0  // last layer and dX0 always take it: dX0 -0.7% cfg2, -5.3% cfg4, dX +0.1% / +2.2%,
+#endif                    // profiles/r20/ab_early_dx.json)
 // whole-line epilogue stores as non-temporal (global_store ... nt): cfg4 forward -6.0%, dX -1.3%, cfg2
 // within 0.2% (profiles/r19/ab_full_lines.json u26); 0 = plain stores
 #ifndef SIREN_NT_STNT
@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     if constexpr (SIREN_NT_SEG2 != 0)
       // EARLY (the next tile's K-tile 1 piece 3 before the epilogue's stores): the fused last layer
       // gains 2.3% (cfg2) / 0.8% (cfg4), the plain forward loses 2.3% at cfg2 (profiles/r20/ab_early.json)
-      pingpong2_tiles<epilogue_stores<Cfg, MODE>(), SIREN_NT_EARLY != 0 || nt_is_hb(MODE)>(
+      pingpong2_tiles<epilogue_stores<Cfg, MODE>(), SIREN_NT_EARLY != 0 || nt_is_hb(MODE) || MODE == NT_DX0>(
           in_range(g_cur), nk, wm, issue, read, mma, set_tiles, tile_end, more);
     else
       pingpong_tiles<epilogue_stores<Cfg, MODE>(), 0xB>(in_range(g_cur), nk, wm, issue, read, mma, set_tiles,
