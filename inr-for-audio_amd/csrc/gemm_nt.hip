@@ -61,6 +61,13 @@
 #ifndef SIREN_NT_STNT
 #define SIREN_NT_STNT 1
 #endif
+// whole-line stores for the Snake / Tanh forward (ping-pong, no HEAD; measurement option, off): Tanh
+// through the 16-KiB scratch (cfg4 -5 to -6%, cfg2 +1 to +2%), Snake (no 16 KiB left) in half-height
+// passes through 1 KiB per wave in the RED region (correct, but its lane exchange spills 128 B: +37%);
+// profiles/r20/ab_act_lines.json.  0 = 16-row pieces
+#ifndef SIREN_NT_ACTLINES
+#define SIREN_NT_ACTLINES 0
+#endif
 
 #ifdef SIREN_DIAG
 #define SIREN_DIAG_ON 1
@@ -123,7 +130,12 @@ struct NtLds {
   // in exactly 160 KiB)
   static constexpr int ST = QS + (nt_is_hb(MODE) ? 0 : 16);
   static constexpr bool LINES = Cfg::PP && (((MODE == NT_FWD || MODE == NT_DX) && !HEAD) ||
-                                            MODE == NT_FWD_HB || MODE == NT_FWD_HB_TANH);
+                                            MODE == NT_FWD_HB || MODE == NT_FWD_HB_TANH ||
+                                            (SIREN_NT_ACTLINES && MODE == NT_FWD_TANH && !HEAD));
+  // the Snake forward without HEAD: 8-row passes through 1 KiB per wave at Cfg::RING (RED, which only
+  // HEAD and the backward modes use)
+  static constexpr bool HALF = Cfg::PP && SIREN_NT_ACTLINES && MODE == NT_FWD_SNAKE && !HEAD;
+  static_assert(!HALF || Cfg::RED >= Cfg::NWAVES * 1024, "half-line scratch");
   static constexpr int SIZE = ST + (LINES ? Cfg::NWAVES * 2048 : 0);
   static_assert(SIZE <= 160 * 1024, "LDS");
 };
@@ -297,9 +309,33 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // wave's first column.
   auto lines_out = [&](h16* out, int row, int col, const uint4 (&v)[Cfg::SN / 2]) {
     static_assert(Cfg::SN == 4, "a wave's row piece is one 128-B line");
-    char* sc = smem + Lay::ST + wave * 2048;
     const int pr = lane & 15, pc = swap16_col(lane) >> 3;  // this lane's piece: row, 16-B chunk
     const int qr = lane >> 3, qc = lane & 7;                // line layout: row (+ 8 q), chunk
+    if constexpr (Lay::HALF) {
+      // rows 8h .. 8h+7 per pass.  No lane may skip a pass's write: the compiler treats the scratch
+      // per lane, and a write under a divergent branch was moved past the other lanes' reads (wrong
+      // rows, gfx950 listing).  So lanes l and l^8 (rows r and r+8) first trade one chunk (DPP
+      // row_ror:8): the low lane then holds both of row r's chunk pairs' pc, the high lane both
+      // 4+pc, one of rows r (pass 0) and r+8 (pass 1) each, and every lane writes once per pass.
+      char* sh = smem + Cfg::RING + wave * 1024;
+      const bool lo = pr < 8;
+      const uint4 send = lo ? v[1] : v[0];
+      uint4 recv;
+      recv.x = __builtin_amdgcn_update_dpp(0, (int)send.x, 0x128, 0xf, 0xf, false);
+      recv.y = __builtin_amdgcn_update_dpp(0, (int)send.y, 0x128, 0xf, 0xf, false);
+      recv.z = __builtin_amdgcn_update_dpp(0, (int)send.z, 0x128, 0xf, 0xf, false);
+      recv.w = __builtin_amdgcn_update_dpp(0, (int)send.w, 0x128, 0xf, 0xf, false);
+      const int r8 = pr & 7, c = (lo ? 0 : 4) + pc;
+      char* wp = sh + r8 * 128 + ((c ^ r8) << 4);
+      const size_t hbase = (size_t)(row - pr + qr) * LD + col + qc * 8;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        *(uint4*)wp = (h == 0) ? (lo ? v[0] : recv) : (lo ? recv : v[1]);
+        stl(out + hbase + (size_t)(8 * h) * LD, *(const uint4*)(sh + qr * 128 + ((qc ^ qr) << 4)));
+      }
+      return;
+    }
+    char* sc = smem + Lay::ST + wave * 2048;
 #pragma unroll
     for (int pp = 0; pp < Cfg::SN / 2; ++pp) {
       const int c = pp * 4 + pc;
@@ -745,11 +781,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           asm volatile("" ::"v"(keep));
           continue;
         }
-        if constexpr (Lay::LINES && MODE == NT_FWD) {
+        if constexpr (Lay::LINES || Lay::HALF) {
           // whole-line stores (lines_out): forward -4.6%, cfg4 -6.5% (static walk,
           // profiles/r19/ab_full_lines.json)
           lines_out(p.Y, mrow0 + j * 16, n0 + wn * TN, yp);
           lines_out(p.C, mrow0 + j * 16, n0 + wn * TN, cpk);
+          if constexpr (MODE == NT_FWD_SNAKE) lines_out(p.E, mrow0 + j * 16, n0 + wn * TN, epk);
           continue;
         }
 #pragma unroll

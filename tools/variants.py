@@ -330,6 +330,9 @@ VARIANTS["hbplain"] = {"gemm_nt.hip": [("""                                     
 VARIANTS["early_dx"] = {"gemm_nt.hip": [("SIREN_NT_EARLY != 0 || nt_is_hb(MODE)>(",
                                          "SIREN_NT_EARLY != 0 || nt_is_hb(MODE) || MODE == NT_DX || MODE == NT_DX0>(")]}
 
+# the Snake / Tanh forward with whole-line stores (SIREN_NT_ACTLINES; the product keeps 16-row pieces)
+VARIANTS["actlines"] = {"gemm_nt.hip": [("#define SIREN_NT_ACTLINES 0", "#define SIREN_NT_ACTLINES 1")]}
+
 
 def build(name: str, extra_defines=()) -> str:
     patches = VARIANTS[name]
