@@ -333,6 +333,12 @@ VARIANTS["early_dx"] = {"gemm_nt.hip": [("SIREN_NT_EARLY != 0 || nt_is_hb(MODE)>
 # the Snake / Tanh forward with whole-line stores (SIREN_NT_ACTLINES; the product keeps 16-row pieces)
 VARIANTS["actlines"] = {"gemm_nt.hip": [("#define SIREN_NT_ACTLINES 0", "#define SIREN_NT_ACTLINES 1")]}
 
+# the first layer's Y0 / C0 stores non-temporal
+VARIANTS["ffnt"] = {"elementwise.hip": [
+    ("    *(h16x8*)(Y0 + m * ld + n) = yv;\n    if constexpr (STORE_C) *(h16x8*)(C0 + m * ld + n) = cv;",
+     "    __builtin_nontemporal_store(yv, (h16x8*)(Y0 + m * ld + n));\n"
+     "    if constexpr (STORE_C) __builtin_nontemporal_store(cv, (h16x8*)(C0 + m * ld + n));")]}
+
 
 def build(name: str, extra_defines=()) -> str:
     patches = VARIANTS[name]
