@@ -149,7 +149,7 @@ hipError_t first_fwd(const float* t, int in_dim, const float* W0, const float* b
   // widths above 2048 run as launches over 1024-column windows (row stride H; every element's
   // arithmetic is its own column's, so the result is the one-launch result)
   const int win = H <= 2048 ? H : 1024;
-  if (H % 8 || 256 % (win / 8) || H % win || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
+  if (H < 8 || H % 8 || 256 % (win / 8) || H % win || in_dim < 1 || in_dim > 2) return hipErrorInvalidValue;
   if ((a0 != nullptr) != (E0 != nullptr) || (a0 && !C0)) return hipErrorInvalidValue;
   const int rpb = 256 / (win / 8);
   const dim3 grid(grid_for(R, rpb, 4096));
@@ -417,7 +417,7 @@ hipError_t head_bwd(const h16* C, const h16* Y, const float* g, const float* w_h
                     const h16* E, float* da_part, hipStream_t s) {
   // widths above 2048: launches over 1024-column windows (row stride H), each column's sums as in one
   const int win = H <= 2048 ? H : 1024;
-  if (R % 128 || win % 4 || H % win || (E && !da_part)) return hipErrorInvalidValue;
+  if (R % 128 || H < 4 || win % 4 || H % win || (E && !da_part)) return hipErrorInvalidValue;
   const bool v8 = win % 8 == 0 && 256 % (win / 8) == 0;
   if (!v8 && 256 % (win / 4)) return hipErrorInvalidValue;
   for (int nb = 0; nb < H; nb += win) {
