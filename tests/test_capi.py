@@ -24,6 +24,18 @@ def test_header_parses():
     assert len(names) >= 24
 
 
+def test_header_constants_match_binding():
+    """The ctypes binding's constants are the header's #defines."""
+    from inr_for_audio_amd import _lib
+    src = open(HEADER).read()
+    defs = dict(re.findall(r"^#define (SIREN_\w+) (\d+)", src, flags=re.M))
+    assert int(defs["SIREN_MAX_HIDDEN"]) == _lib.MAX_HIDDEN
+    assert int(defs["SIREN_MAX_INNER"]) == _lib.MAX_INNER
+    assert int(defs["SIREN_ROW_TILE"]) == _lib.ROW_TILE
+    assert int(defs["SIREN_TILEQ_INTS"]) == _lib.TILEQ_INTS
+    assert int(defs["SIREN_ABI_VERSION"]) == _lib.ABI_VERSION
+
+
 def test_library_exports_every_declared_symbol(lib):
     for name in declared():
         assert hasattr(lib, name), name
