@@ -61,13 +61,6 @@
 #ifndef SIREN_NT_STNT
 #define SIREN_NT_STNT 1
 #endif
-// whole-line stores for the Snake / Tanh forward (ping-pong, no HEAD; measurement option, off): Tanh
-// through the 16-KiB scratch (cfg4 -5 to -6%, cfg2 +1 to +2%), Snake (no 16 KiB left) in half-height
-// passes through 1 KiB per wave in the RED region (correct, but its lane exchange spills 128 B: +37%);
-// profiles/r20/ab_act_lines.json.  0 = 16-row pieces
-#ifndef SIREN_NT_ACTLINES
-#define SIREN_NT_ACTLINES 0
-#endif
 
 #ifdef SIREN_DIAG
 #define SIREN_DIAG_ON 1
@@ -117,7 +110,11 @@ using NtLargePP = NtCfg<256, 256, 2, 4, 64, 2, true>;
 // LDS layout of one kernel instance: the ring, the epilogue reduction scratch, then only the
 // per-column vectors its mode needs (bias for the forward modes, head weights with HEAD, Snake
 // a), then the tile-queue slots.
-template <class Cfg, int MODE, bool HEAD>
+// ACTL: the Snake / Tanh forward (ping-pong, no HEAD) with whole-line stores -- Tanh through the 16-KiB
+// scratch, Snake (no 16 KiB left) in 8-row passes through 1 KiB per wave in the RED region.  gemm_nt
+// takes it at K <= 512 only: at train()'s default width 256 Snake -19%, Tanh -16%; at 512 -3% / -6%;
+// at 1024 +4.5% / +1.3% (profiles/r20/ab_act_lines.json, bit-identical)
+template <class Cfg, int MODE, bool HEAD, bool ACTL = false>
 struct NtLds {
   static constexpr int BIAS = Cfg::RING + Cfg::RED;
   static constexpr int HW = BIAS + (nt_is_fwd(MODE) ? Cfg::VEC : 0);
@@ -131,12 +128,13 @@ struct NtLds {
   static constexpr int ST = QS + (nt_is_hb(MODE) ? 0 : 16);
   static constexpr bool LINES = Cfg::PP && (((MODE == NT_FWD || MODE == NT_DX) && !HEAD) ||
                                             MODE == NT_FWD_HB || MODE == NT_FWD_HB_TANH ||
-                                            (SIREN_NT_ACTLINES && MODE == NT_FWD_TANH && !HEAD));
+                                            (ACTL && MODE == NT_FWD_TANH && !HEAD));
   // the Snake forward without HEAD: 8-row passes through 1 KiB per wave at Cfg::RING (RED, which only
   // HEAD and the backward modes use)
-  static constexpr bool HALF = Cfg::PP && SIREN_NT_ACTLINES && MODE == NT_FWD_SNAKE && !HEAD;
+  static constexpr bool HALF = Cfg::PP && ACTL && MODE == NT_FWD_SNAKE && !HEAD;
   static_assert(!HALF || Cfg::RED >= Cfg::NWAVES * 1024, "half-line scratch");
-  static constexpr int SIZE = ST + (LINES ? Cfg::NWAVES * 2048 : 0);
+  static constexpr int DM = ST;  // HALF: 64 lanes x 32 B of write-only slots
+  static constexpr int SIZE = ST + (LINES ? Cfg::NWAVES * 2048 : 0) + (HALF ? 64 * 32 : 0);
   static_assert(SIZE <= 160 * 1024, "LDS");
 };
 
@@ -194,11 +192,11 @@ constexpr int epilogue_stores() {
 }
 
 // QUEUE (ping-pong K-loop only): tiles from the dynamic queue p.tileq instead of the static walk
-template <class Cfg, int MODE, bool HEAD, bool QUEUE = false>
+template <class Cfg, int MODE, bool HEAD, bool QUEUE = false, bool ACTL = false>
 __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, BK = Cfg::BK, WN = Cfg::WN;
   constexpr int TM = Cfg::TM, TN = Cfg::TN, SM = Cfg::SM, SN = Cfg::SN;
-  using Lay = NtLds<Cfg, MODE, HEAD>;
+  using Lay = NtLds<Cfg, MODE, HEAD, ACTL>;
   __shared__ __attribute__((aligned(16))) char smem[Lay::SIZE];
 
   const int tid = threadIdx.x;
@@ -314,23 +312,21 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     if constexpr (Lay::HALF) {
       // rows 8h .. 8h+7 per pass.  No lane may skip a pass's write: the compiler treats the scratch
       // per lane, and a write under a divergent branch was moved past the other lanes' reads (wrong
-      // rows, gfx950 listing).  So lanes l and l^8 (rows r and r+8) first trade one chunk (DPP
-      // row_ror:8): the low lane then holds both of row r's chunk pairs' pc, the high lane both
-      // 4+pc, one of rows r (pass 0) and r+8 (pass 1) each, and every lane writes once per pass.
+      // rows, gfx950 listing; a DPP exchange that avoids it spilled).  So every lane writes both its
+      // chunks in both passes, those of the other pass's rows to slots nobody reads (Lay::DM,
+      // shared by the block's waves: garbage by design).
       char* sh = smem + Cfg::RING + wave * 1024;
-      const bool lo = pr < 8;
-      const uint4 send = lo ? v[1] : v[0];
-      uint4 recv;
-      recv.x = __builtin_amdgcn_update_dpp(0, (int)send.x, 0x128, 0xf, 0xf, false);
-      recv.y = __builtin_amdgcn_update_dpp(0, (int)send.y, 0x128, 0xf, 0xf, false);
-      recv.z = __builtin_amdgcn_update_dpp(0, (int)send.z, 0x128, 0xf, 0xf, false);
-      recv.w = __builtin_amdgcn_update_dpp(0, (int)send.w, 0x128, 0xf, 0xf, false);
-      const int r8 = pr & 7, c = (lo ? 0 : 4) + pc;
-      char* wp = sh + r8 * 128 + ((c ^ r8) << 4);
+      char* dm = smem + Lay::DM + lane * 32;
+      const int r8 = pr & 7;
       const size_t hbase = (size_t)(row - pr + qr) * LD + col + qc * 8;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        *(uint4*)wp = (h == 0) ? (lo ? v[0] : recv) : (lo ? recv : v[1]);
+        const bool mine = (pr >> 3) == h;
+#pragma unroll
+        for (int pp = 0; pp < Cfg::SN / 2; ++pp) {
+          const int c = pp * 4 + pc;
+          *(uint4*)(mine ? sh + r8 * 128 + ((c ^ r8) << 4) : dm + pp * 16) = v[pp];
+        }
         stl(out + hbase + (size_t)(8 * h) * LD, *(const uint4*)(sh + qr * 128 + ((qc ^ qr) << 4)));
       }
       return;
@@ -1169,7 +1165,7 @@ static int stream_cus(hipStream_t s) {
 static int g_hb_per_cu[3][64] = {};
 static bool hb_coresident(int mode, int grid, hipStream_t s);
 
-template <class Cfg, int MODE, bool HEAD>
+template <class Cfg, int MODE, bool HEAD, bool ACTL = false>
 static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent) {
   // the static ping-pong schedule assumes an even number (>= 2) of K-tiles per tile
   if (Cfg::PP && (p_in.K % (2 * Cfg::BK) != 0 || !persistent)) return hipErrorInvalidValue;
@@ -1214,11 +1210,11 @@ static hipError_t launch_nt(const NtParams& p_in, hipStream_t s, bool persistent
       // (graph capture records the memset as a node before the kernel)
       const hipError_t e = hipMemsetAsync(p.tileq, 0, kQueueSet * sizeof(int), s);
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD, true>), dim3(grid), dim3(Cfg::THREADS), 0, s, p);
+      hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD, true, ACTL>), dim3(grid), dim3(Cfg::THREADS), 0, s, p);
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD>), dim3(grid), dim3(Cfg::THREADS), 0, s, p);
+  hipLaunchKernelGGL((gemm_nt_kernel<Cfg, MODE, HEAD, false, ACTL>), dim3(grid), dim3(Cfg::THREADS), 0, s, p);
   return hipGetLastError();
 }
 
@@ -1261,11 +1257,13 @@ template <class Cfg>
 static hipError_t dispatch_act(int mode, bool head, const NtParams& p, hipStream_t s, bool persistent) {
   switch (mode) {
     case NT_FWD_SNAKE:
-      return head ? launch_nt<Cfg, NT_FWD_SNAKE, true>(p, s, persistent)
-                  : launch_nt<Cfg, NT_FWD_SNAKE, false>(p, s, persistent);
+      if (head) return launch_nt<Cfg, NT_FWD_SNAKE, true>(p, s, persistent);
+      return (Cfg::PP && p.K <= 512) ? launch_nt<Cfg, NT_FWD_SNAKE, false, true>(p, s, persistent)
+                                     : launch_nt<Cfg, NT_FWD_SNAKE, false>(p, s, persistent);
     case NT_FWD_TANH:
-      return head ? launch_nt<Cfg, NT_FWD_TANH, true>(p, s, persistent)
-                  : launch_nt<Cfg, NT_FWD_TANH, false>(p, s, persistent);
+      if (head) return launch_nt<Cfg, NT_FWD_TANH, true>(p, s, persistent);
+      return (Cfg::PP && p.K <= 512) ? launch_nt<Cfg, NT_FWD_TANH, false, true>(p, s, persistent)
+                                     : launch_nt<Cfg, NT_FWD_TANH, false>(p, s, persistent);
     case NT_DX_SNAKE: return launch_nt<Cfg, NT_DX_SNAKE, false>(p, s, persistent);
   }
   return hipErrorInvalidValue;

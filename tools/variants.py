@@ -330,8 +330,8 @@ VARIANTS["hbplain"] = {"gemm_nt.hip": [("""                                     
 VARIANTS["early_dx"] = {"gemm_nt.hip": [("SIREN_NT_EARLY != 0 || nt_is_hb(MODE)>(",
                                          "SIREN_NT_EARLY != 0 || nt_is_hb(MODE) || MODE == NT_DX || MODE == NT_DX0>(")]}
 
-# the Snake / Tanh forward with whole-line stores (SIREN_NT_ACTLINES; the product keeps 16-row pieces)
-VARIANTS["actlines"] = {"gemm_nt.hip": [("#define SIREN_NT_ACTLINES 0", "#define SIREN_NT_ACTLINES 1")]}
+# the Snake / Tanh forward with 16-row store pieces at every K (the product takes whole lines at K <= 512)
+VARIANTS["actplain"] = {"gemm_nt.hip": [("(Cfg::PP && p.K <= 512)", "(Cfg::PP && p.K <= 0)")]}
 
 # the first layer's Y0 / C0 stores non-temporal
 VARIANTS["ffnt"] = {"elementwise.hip": [
