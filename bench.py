@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
 import re
@@ -49,8 +50,8 @@ def cpu_model() -> str:
 
 
 KIND_MATCH = {  # profile kind -> (kernel-name substring, (MODE, HEAD) of gemm_nt_kernel or None)
-    # gemm_nt_kernel<Cfg, MODE, HEAD[, QUEUE]>: statically walked (QUEUE false) or from the
-    # dynamic tile queue (gemm_nt.hip); QUEUE is not part of the kind
+    # gemm_nt_kernel<Cfg, MODE, HEAD[, QUEUE[, ACTL]]>: statically walked (QUEUE false) or from the
+    # dynamic tile queue (gemm_nt.hip), whole-line Snake / Tanh stores (ACTL); neither is part of the kind
     "inner_fwd": ("gemm_nt_kernel", ("0", "false")),
     "bwd_dx": ("gemm_nt_kernel", ("1", "false")),
     "bwd_dx0": ("gemm_nt_kernel", ("2", "false")),
@@ -58,7 +59,7 @@ KIND_MATCH = {  # profile kind -> (kernel-name substring, (MODE, HEAD) of gemm_n
     # NT_FWD_HB: the last layer fused with the head, the loss gradient and the head backward
     "head_fwd": ("gemm_nt_kernel", ("7", "true")),
 }
-_NT_ARGS = re.compile(r"gemm_nt_kernel<siren::NtCfg<[^>]*>, (\d+), (true|false)(?:, (?:true|false))?>")
+_NT_ARGS = re.compile(r"gemm_nt_kernel<siren::NtCfg<[^>]*>, (\d+), (true|false)(?:, (?:true|false)){0,2}>")
 
 
 def kind_match(kind: str, kernel_name: str) -> bool:
@@ -117,7 +118,37 @@ CONFIGS = {  # name: (hidden, layers, in_dim, coords per GPU, omega0, grid heigh
     "cfg2": (1024, 5, 1, 1 << 20, 3000.0, None),
     "cfg3": (1024, 6, 2, 3_600_000, 3000.0, 1_800_000),
     "cfg4": (512, 5, 2, 1024 * 215, 1000.0, 1024),
+    # the reference's own live workload (run.py:466: width 256, a first SineLayer at omega 22000 then
+    # num_sine=0, num_snake=4, 10 s of 44.1 kHz audio) and train()'s default stack (run.py:30:
+    # num_sine=2, num_snake=2, width 256, omega 22000, a_initial 0.5) on the same 10 s
+    "live": (256, 5, 1, 441_000, 22000.0, None),
+    "default": (256, 5, 1, 441_000, 22000.0, None),
 }
+# hidden-layer kinds (num_sine, num_snake) of the configs that are not all-sine
+STACKS = {"live": (0, 4), "default": (2, 2)}
+A_INITIAL = 0.5  # run.py:30
+
+
+def siren_bytes_per_row(acts, H, in_dim=1):
+    """Algorithmic HBM bytes per coordinate of one fused training step, per launch kind (fp16
+    activations, 2 B per element; weights, partials and slabs are O(H^2) per launch and left out).
+    acts: 'sine' / 'snake' per hidden layer, the last one fused with the head (NT_FWD_HB*):
+      first_fwd   reads the coordinate, writes Y0, C0
+      inner_fwd   layer i < L-1: reads X_i, writes Y, C (+ E for Snake)
+      head_fwd    layer L-1 + head + loss gradient + head backward: reads X, writes dZ_{L-1}
+                  (a Snake's E goes to HBM and back inside the launch: scratch, not counted)
+      bwd_dx      into layer i-1, i = L-1 .. 1: reads dZ_i, C_i (+ E_i below a Snake), writes dZ_{i-1}
+      bwd_dx0     into the first layer: reads dZ_0, C_0 (partials only)
+      bwd_dw      layer i: reads Y_i and dZ_i"""
+    e = 2 * H
+    L = len(acts)
+    by = {"first_fwd": 4 * in_dim + 2 * e, "inner_fwd": 0, "head_fwd": 2 * e, "bwd_dx": 0, "bwd_dx0": 2 * e,
+          "bwd_dw": 2 * e * L}
+    for i in range(L - 1):
+        by["inner_fwd"] += e + e * (3 if acts[i] == "snake" else 2)
+    for i in range(L - 1, 0, -1):
+        by["bwd_dx"] += e * (4 if acts[i - 1] == "snake" else 3)
+    return by
 
 
 PEAK_F32_TFLOPS = 157.3   # MI355X dense fp32 (f32-input MFMA = the vector rate; MI355X_MICROARCH.md)
@@ -399,13 +430,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=sorted(CONFIGS) + ["cfg5"], default="cfg2")
+    ap.add_argument("--config", choices=sorted(CONFIGS) + ["cfg5"], default="cfg2",
+                    help="cfg2 (default) .. cfg5: BASELINE.json's configs; live / default: the reference's run.py:466 "
+                         "workload / train()'s default stack (width 256, Snake layers)")
     ap.add_argument("--hidden", type=int, default=None, help="override the config's width")
     ap.add_argument("--layers", type=int, default=None, help="SIREN L: sine layers incl. the first")
     ap.add_argument("--coords", type=int, default=None, help="coordinates per GPU (weak scaling), or the global "
                     "batch with --strong")
     ap.add_argument("--strong", action="store_true", help="strong scaling (cfg2 / cfg5): the global batch "
                     "(--coords, default the config's) is fixed and split over the ranks")
+    ap.add_argument("--emulate-ranks", type=int, default=None, help="one process runs rank 0's shard of a "
+                    "G-rank job (per-rank compute of a scaling curve on one GPU; n_total stays global; with "
+                    "--strong the global batch is split G ways); `value` is then this rank's coord-samples/s")
     ap.add_argument("--omega0", type=float, default=None)
     ap.add_argument("--micro-batch", type=int, default=None, help="rows per fused micro-batch "
                     "(default: the whole per-GPU batch)")
@@ -418,7 +454,7 @@ def main():
     args = ap.parse_args()
 
     import __graft_entry__ as ge
-    ge.build()
+    ge.build(diag=False)  # the SIREN_DIAG test library is never loaded here
     from inr_for_audio_amd import _lib
     from inr_for_audio_amd.engine import SirenEngine, round_up
     from inr_for_audio_amd.models import SirenWithSnakeTanh
@@ -435,6 +471,11 @@ def main():
         torch.cuda.set_device(dev)
         dist.init_process_group(args.backend)
     lib = _lib.load()
+    ranks = world
+    if args.emulate_ranks:
+        if world != 1 or args.config not in ("cfg2", "live", "default"):
+            raise SystemExit("--emulate-ranks: one process, a 1-D (linspace) config")
+        ranks = args.emulate_ranks
     if args.config == "cfg5":
         return run_kan(args, world, rank, dev, dist, lib, _lib)
 
@@ -444,8 +485,8 @@ def main():
     omega0 = args.omega0 if args.omega0 is not None else cfg_w0
     stream = torch.cuda.current_stream(dev).cuda_stream
     if in_dim == 1:
-        per_gpu = round_up(-(-(args.coords or cfg_coords) // world) if args.strong else (args.coords or cfg_coords), 128)
-        n_total = per_gpu * world
+        per_gpu = round_up(-(-(args.coords or cfg_coords) // ranks) if args.strong else (args.coords or cfg_coords), 128)
+        n_total = per_gpu * ranks
         # this rank's shard of the global linspace grid, generated on device (bit-exact linspace)
         coords = torch.empty(per_gpu, 1, dtype=torch.float32, device=dev)
         _lib.check(lib.siren_coords_fill(coords.data_ptr(), per_gpu, rank * per_gpu, n_total, stream),
@@ -475,7 +516,15 @@ def main():
             + 0.2 * torch.sin(7100.0 * t + 0.5 * ch)
 
     torch.manual_seed(0)
-    model = SirenWithSnakeTanh(in_dim, 1, H, L, 0, 0, first_omega_0=omega0, hidden_omega_0=30.0)
+    n_sine, n_snake = STACKS.get(args.config, (L, 0))
+    if args.config in STACKS:
+        L = n_sine + n_snake
+        layers_kind = ["sine"] * n_sine + ["snake"] * n_snake
+        model = SirenWithSnakeTanh(in_dim, 1, H, n_sine, n_snake, 0, first_omega_0=omega0, hidden_omega_0=30.0,
+                                   a_initial=A_INITIAL)
+    else:
+        layers_kind = ["sine"] * L
+        model = SirenWithSnakeTanh(in_dim, 1, H, L, 0, 0, first_omega_0=omega0, hidden_omega_0=30.0)
     eng = SirenEngine(model, coords, target, n_total=n_total, micro_batch=args.micro_batch or per_gpu,
                       hist_cap=args.warmup + args.steps + 6, device=dev)
     for _ in range(args.warmup):
@@ -484,7 +533,12 @@ def main():
 
     gemm_all = ("inner_fwd", "head_fwd", "bwd_dx", "bwd_dw", "bwd_dx0")
 
+    bpr = siren_bytes_per_row(layers_kind, H, in_dim) if args.config in STACKS else None
+
     def pick(pr, n):
+        # the width-256 Snake stacks are HBM-bound: the roofline names the kind with the most time per step
+        if bpr is not None:
+            return max((k for k in bpr if pr[k][1]), key=lambda k: pr[k][0])
         # pinned to north_star's "inner GEMM": the SineLayer forward (models.py:114-115), which is
         # also the kind with the most time per step by rocprof (3 launches at cfg2).  The forward,
         # dX and dW kinds sit within 3 % of each other per step, so choosing by time in the untimed
@@ -519,7 +573,7 @@ def main():
     headline = args.config == "cfg2" and H == 1024 and L == 4 and per_gpu == 1 << 20 and eng.n_micro == 1
     traffic, traffic_src = pmc_traffic(dom) if headline else (None, None)
     ms_per_step = elapsed / args.steps * 1e3
-    value = n_total * args.steps / elapsed
+    value = (n_total if ranks == world else per_gpu) * args.steps / elapsed
     layers = L + 1
     result = {
         "metric": METRIC, "value": value, "unit": "coord-samples/s", "n_gpus": world,
@@ -528,7 +582,8 @@ def main():
         "vs_baseline": None, "dtype": "fp16",
         "data": f"synthetic tone mix on the {grid}; random-init weights (seed 0)",
         "config": {"workload": f"{args.config}: SIREN {layers}x{H} (in = {in_dim}) full-batch fit step, "
-                               f"{per_gpu} coords/GPU",
+                               f"{per_gpu} coords/GPU" + (f" (rank 0 of {ranks} emulated, {n_total} global)"
+                                                          if ranks != world else ""),
                    "name": args.config, "global_batch": n_total, "coords_per_gpu": per_gpu, "hidden": H,
                    "layers": layers, "in_features": in_dim, "omega0": omega0, "hidden_omega": 30.0,
                    "micro_batches_per_gpu": eng.n_micro, "parallelism": f"dp{world}",
@@ -558,6 +613,38 @@ def main():
         "final_loss": loss,
         "fp16_overflow_steps": eng.guard_state()["overflows"],
     }
+    if ranks != world:
+        # fill of the persistent GEMM grids at this shard: 256 x 256 tiles over the CUs
+        tiles = (round_up(per_gpu // eng.n_micro, 256) // 256) * (H // 256)
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        waves = tiles / cus
+        result["emulated"] = {
+            "ranks": ranks, "rank": 0, "coords_this_rank": per_gpu, "global_batch": n_total,
+            "value_is": "this rank's coord-samples/s (the job's would be ranks x value with no exchange cost)",
+            "ideal_job_value": value * ranks, "gemm_tiles_per_launch": tiles, "cus": cus,
+            "waves": waves, "wave_tail_frac": (math.ceil(waves) - waves) / math.ceil(waves)}
+        result["scaling"] = "strong" if args.strong else "weak"
+    if bpr is not None:
+        # HBM roofline (width 256: 2 H^2 flop per row against >= 8 H bytes, far below the MFMA ridge)
+        fused = prof["head_fwd"][1] > 0
+        for k, b in bpr.items():
+            if k in kernels:
+                kernels[k]["bytes_per_step"] = b * per_gpu
+                kernels[k]["gbs"] = b * per_gpu / (kernels[k]["ms_per_step"] * 1e-3) / 1e9
+        step_bytes = sum(bpr.values()) * per_gpu
+        result["config"]["stack"] = {"first": "sine", "hidden": layers_kind, "a_initial": A_INITIAL,
+                                     "reference": "run.py:466" if args.config == "live" else "run.py:30 defaults"}
+        result["roofline"] = {
+            "bound": "hbm", "kernel": dom, "kernel_choice": "the kind with the most time per step (HBM-bound stack)",
+            "achieved": kernels[dom]["gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": kernels[dom]["gbs"] / PEAK_HBM_GBS, "traffic": None,
+            "algorithmic_bytes_per_row": bpr[dom] / kernels[dom]["launches_per_step"],
+            "rows_per_launch": per_gpu / eng.n_micro, "head_fused": fused,
+            "mfma": {"achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_BF16_TFLOPS}}
+        result["step_hbm_frac"] = step_bytes / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS
+        result["step_algorithmic_bytes"] = step_bytes
+        result["bytes_per_row_by_kind"] = bpr
     if dist is not None:
         result["dist"] = dp_report(eng, args, dev, dist)
     if world == 1 and args.config == "cfg2" and not args.no_recon_snr:
@@ -569,11 +656,13 @@ def main():
         # headline (cfg2) times both counts and reports the faster, the sweep kept beside it; the
         # other configs time the share only (the thrashing leg costs minutes and never wins).
         from oracle import torch_cpu_step
+        n_cpu = args.cpu_coords if args.config not in STACKS else 4 * args.cpu_coords  # width 256: 16x less work/row
         what = (f"torch-CPU fp32 port of run.py's step (oracle/torch_cpu_step.py), SIREN {layers}x{H} "
-                f"(in = {in_dim}), {args.cpu_coords} coords")
+                f"(in = {in_dim}; hidden {'/'.join(layers_kind)}), {n_cpu} coords")
         result["cpu_baseline"] = cpu_baseline_sweep(
-            lambda threads, steps: torch_cpu_step.time_steps(args.cpu_coords, H, L, steps=steps, threads=threads,
-                                                             omega0=omega0, in_dim=in_dim),
+            lambda threads, steps: torch_cpu_step.time_steps(n_cpu, H, n_sine, steps=steps, threads=threads,
+                                                             omega0=omega0, in_dim=in_dim, n_snake=n_snake,
+                                                             a0=A_INITIAL),
             args, what, share_only=args.config != "cfg2")
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -174,9 +174,9 @@ typedef struct siren_batch {
    * taken from those partials; the range guard catches a step whose |g| outgrew it).  0: a Snake
    * last layer runs unfused.  Sine / Tanh last layers ignore it. */
   int32_t head_scale_prev;
-  /* range guard (NULL: fixed headroom 6, no overflow recovery).  ABI 12: not const -- a fused last
-   * layer whose hand-off wait times out counts it in guard->stalls (with no guard it can only turn
-   * the band's loss into NaN) */
+  /* range guard (NULL: fixed headroom 6, no overflow recovery, and the last layer runs unfused).
+   * ABI 12: not const -- a fused last layer whose hand-off wait times out counts it in
+   * guard->stalls, which voids the step */
   siren_guard* guard;
   int32_t* tileq;            /* SIREN_TILEQ_INTS ints of tile-queue counters on the device of the
                                 activations (NULL: the forward GEMM's static tile walk) */

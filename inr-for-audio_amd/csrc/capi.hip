@@ -139,6 +139,9 @@ int g_head_fuse = 1;
 bool head_fused(const siren_net* n, const siren_batch* b, hipStream_t s) {
   const int act = n->act[n->n_inner - 1];
   if (!g_head_fuse || (act == SIREN_ACT_SNAKE && !b->head_scale_prev)) return false;
+  // the hand-off's timeout is only made loud through the guard's stall word: without a guard a
+  // timed-out band would reach Adam as a NaN gradient, so a guard-less batch runs unfused
+  if (!b->guard) return false;
   return gemm_nt_head_fusable(b->rows, n->hidden, s, hb_mode(act));
 }
 

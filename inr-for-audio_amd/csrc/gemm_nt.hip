@@ -113,7 +113,9 @@ using NtLargePP = NtCfg<256, 256, 2, 4, 64, 2, true>;
 // ACTL: the Snake / Tanh forward (ping-pong, no HEAD) with whole-line stores -- Tanh through the 16-KiB
 // scratch, Snake (no 16 KiB left) in 8-row passes through 1 KiB per wave in the RED region.  gemm_nt
 // takes it at K <= 512 only: at train()'s default width 256 Snake -19%, Tanh -16%; at 512 -3% / -6%;
-// at 1024 +4.5% / +1.3% (profiles/r20/ab_act_lines.json, bit-identical)
+// at 1024 +4.5% / +1.3% (profiles/r20/ab_act_lines.json, bit-identical).  The dX into a Snake layer
+// (NT_DX_SNAKE) takes the same K <= 512 switch for whole-line dZ stores through the 16-KiB scratch
+// (width 256 -1.2%, 512 -7.1%, bit-identical; profiles/r22/ab_dxsl_*.json)
 template <class Cfg, int MODE, bool HEAD, bool ACTL = false>
 struct NtLds {
   static constexpr int BIAS = Cfg::RING + Cfg::RED;
@@ -128,7 +130,7 @@ struct NtLds {
   static constexpr int ST = QS + (nt_is_hb(MODE) ? 0 : 16);
   static constexpr bool LINES = Cfg::PP && (((MODE == NT_FWD || MODE == NT_DX) && !HEAD) ||
                                             MODE == NT_FWD_HB || MODE == NT_FWD_HB_TANH ||
-                                            (ACTL && MODE == NT_FWD_TANH && !HEAD));
+                                            (ACTL && (MODE == NT_FWD_TANH || MODE == NT_DX_SNAKE) && !HEAD));
   // the Snake forward without HEAD: 8-row passes through 1 KiB per wave at Cfg::RING (RED, which only
   // HEAD and the backward modes use)
   static constexpr bool HALF = Cfg::PP && ACTL && MODE == NT_FWD_SNAKE && !HEAD;
@@ -181,6 +183,8 @@ constexpr unsigned kHeadPending = 0xFFFFFFFFu;
 // range guard's stall word (NtParams::stall -> GuardState::stalls), which voids the step: the
 // update kernels skip it and the engine raises (include/siren_hip.h siren_guard)
 constexpr int kHeadSpinLimit = 1 << 25;
+// a waiting thread re-reads the stall word every kStallCheck polls (power of two)
+constexpr int kStallCheck = 256;
 
 // store instructions every wave's epilogue issues (lower bound; see mfma_pipeline_tiles)
 template <class Cfg, int MODE>
@@ -327,7 +331,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           const int c = pp * 4 + pc;
           *(uint4*)(mine ? sh + r8 * 128 + ((c ^ r8) << 4) : dm + pp * 16) = v[pp];
         }
-        stl(out + hbase + (size_t)(8 * h) * LD, *(const uint4*)(sh + qr * 128 + ((qc ^ qr) << 4)));
+        // the exchange is across lanes: no LDS access moves over these (LDS is in order within a
+        // wave, so they cost no wait; the ordering no longer rests on how the select is written)
+        __builtin_amdgcn_wave_barrier();
+        const uint4 line = *(const uint4*)(sh + qr * 128 + ((qc ^ qr) << 4));
+        __builtin_amdgcn_wave_barrier();
+        stl(out + hbase + (size_t)(8 * h) * LD, line);
       }
       return;
     }
@@ -337,12 +346,17 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       const int c = pp * 4 + pc;
       *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = v[pp];
     }
+    __builtin_amdgcn_wave_barrier();  // cross-lane exchange: the reads stay after every lane's writes
     const size_t fbase = (size_t)(row - pr + qr) * LD + col + qc * 8;
+    uint4 line[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int r = qr + 8 * q;
-      stl(out + fbase + (size_t)(8 * q) * LD, *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4)));
+      line[q] = *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4));
     }
+    __builtin_amdgcn_wave_barrier();  // ... and the next output's writes after these reads
+#pragma unroll
+    for (int q = 0; q < 2; ++q) stl(out + fbase + (size_t)(8 * q) * LD, line[q]);
   };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
@@ -537,6 +551,14 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               if (++polls > p.spin_limit) {
                 u = 0x7fc00000u;
                 if (p.stall) __hip_atomic_fetch_add(p.stall, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+              // fail fast: once any wait of this step (this launch or an earlier micro-batch's) has given
+              // up, the step is void already -- every other wait stops within kStallCheck polls instead
+              // of spending its own whole limit (the stall word is sticky until the host clears it)
+              if ((polls & (kStallCheck - 1)) == 0 && p.stall &&
+                  __hip_atomic_load(p.stall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                u = 0x7fc00000u;
                 break;
               }
               __builtin_amdgcn_s_sleep(1);
@@ -847,6 +869,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       };
       // the 16-B piece (row subtile j, column pair pp) from its Cprev (and Eprev) piece.  Each column
       // partial sums its rows in order 0 .. SM-1 whatever order the pieces go in
+      // NT_DX_SNAKE with whole-line stores (Lay::LINES): a row piece's two 16-B pieces (the Snake batches
+      // below take both column pairs of a row back to back, pair 1 last)
+      uint4 dzrow[SN / 2];
       auto piece = [&](auto jc, auto ppc, const uint4& cpv, const uint4& epv) {
         constexpr int j = decltype(jc)::value, pp = decltype(ppc)::value;
         const size_t rowoff = (size_t)(mrow0 + j * 16) * LD;
@@ -878,8 +903,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           });
           dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
         }
-        if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE)
+        if constexpr (MODE == NT_DX_SNAKE && Lay::LINES) {
+          dzrow[pp] = swap16_pair(dzp[0], dzp[1]);
+          if constexpr (pp == SN / 2 - 1) lines_out(p.dZ, mrow0 + j * 16, n0 + wn * TN, dzrow);
+        } else if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE) {
           st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+        }
       };
       if constexpr (HAS_E) {
         // batches of EB rows, both column pairs of a row back to back: the two 64-B halves of each
@@ -1051,13 +1080,20 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       bases(g_cur, x0, w0);
       bases(in_range(g_next) ? g_next : g_cur, x1, w1);
     };
+    // the piece's second 8 rows: 8 rows further in the operand, 1 KiB further in LDS
+    // (urow[PC][1] = urow[PC][0] + 8 rows, pdst[PC][1] = pdst[PC][0] + 1 KiB: glds16x2o_asm_s's offset:1024)
+    const unsigned lane_src8 = lane_src + (unsigned)(16 * K) - 1024u;
     auto issue = [&](int sel, int kt, int slot, auto pcc) {
       constexpr int PC = decltype(pcc)::value;
       const h16* src = ((PC & 1) ? (sel ? x1 : x0) : (sel ? w1 : w0)) + kt * BK;
       const char* dst = smem + slot * Cfg::STAGE;
+      if constexpr (SIREN_GLDS_PAIR != 0) {
+        glds16x2o_asm_s(lane_src, lane_src8, (const char*)src + urow[PC][0], lds_addr(dst + pdst[PC][0]));
+      } else {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        glds16_asm_s(lane_src, (const char*)src + urow[PC][j], lds_addr(dst + pdst[PC][j]));
+        for (int j = 0; j < 2; ++j)
+          glds16_asm_s(lane_src, (const char*)src + urow[PC][j], lds_addr(dst + pdst[PC][j]));
+      }
     };
     h16x8 xf[4][2], wf0[2][2], wf1[2][2];
     auto rd_w = [&](h16x8 (&wf)[2][2], const char* ws, int n_off) {
@@ -1264,7 +1300,9 @@ static hipError_t dispatch_act(int mode, bool head, const NtParams& p, hipStream
       if (head) return launch_nt<Cfg, NT_FWD_TANH, true>(p, s, persistent);
       return (Cfg::PP && p.K <= 512) ? launch_nt<Cfg, NT_FWD_TANH, false, true>(p, s, persistent)
                                      : launch_nt<Cfg, NT_FWD_TANH, false>(p, s, persistent);
-    case NT_DX_SNAKE: return launch_nt<Cfg, NT_DX_SNAKE, false>(p, s, persistent);
+    case NT_DX_SNAKE:
+      return (Cfg::PP && p.K <= 512) ? launch_nt<Cfg, NT_DX_SNAKE, false, true>(p, s, persistent)
+                                     : launch_nt<Cfg, NT_DX_SNAKE, false>(p, s, persistent);
   }
   return hipErrorInvalidValue;
 }

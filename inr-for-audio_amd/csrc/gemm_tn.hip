@@ -169,16 +169,34 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_tn_kernel(TnParams p) {
     if constexpr (Cfg::PP == 2) {
       // segment A = k32 half 0 (pieces 0, 1), B = half 1 (pieces 2, 3); all 8 i-subtiles each
       h16x8 a8[8], b4[4];
+      // SIREN_GLDS_PAIR (siren_common.h): a piece's two DMAs (rows r and r + 2, 1 KiB apart in LDS) from one
+      // wave-uniform base in SGPRs and 32-bit lane byte offsets, one statement per piece
+      unsigned yb0[2], yb1[2], zb0[2], zb1[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        yb0[kk] = (unsigned)yo[kk][0] * 2u;
+        yb1[kk] = (unsigned)yo[kk][1] * 2u - 1024u;  // glds16x2o_asm_s's offset:1024
+        zb0[kk] = (unsigned)zo[kk][0] * 2u;
+        zb1[kk] = (unsigned)zo[kk][1] * 2u - 1024u;
+      }
       auto issue2 = [&](int kt, int slot, auto pcc) {
         constexpr int PC = decltype(pcc)::value, KK = PC >> 1;
         const int ks = ks_begin + min(kt, nkl - 1);  // past the slice: a consumed piece re-read
         const char* dst = smem + slot * Cfg::STAGE;
+        if constexpr (SIREN_GLDS_PAIR != 0) {
+          static_assert(2 * Cfg::YROW == 1024 && 2 * Cfg::ZROW == 1024, "a piece's halves are 1 KiB apart");
+          const bool y = (PC & 1) != 0;
+          const void* base = y ? (const void*)(p.Y + (size_t)ks * BK * p.Hin) : (const void*)(p.dZ + (size_t)ks * BK * p.Hout);
+          const unsigned lds = lds_addr(dst + (y ? 0 : Cfg::YBYTES) + po[KK][0]);
+          glds16x2o_asm_s(y ? yb0[KK] : zb0[KK], y ? yb1[KK] : zb1[KK], base, lds);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if constexpr ((PC & 1) != 0)
-            glds16_asm(p.Y + (size_t)ks * BK * p.Hin + yo[KK][j], lds_addr(dst + po[KK][j]));
-          else
-            glds16_asm(p.dZ + (size_t)ks * BK * p.Hout + zo[KK][j], lds_addr(dst + Cfg::YBYTES + po[KK][j]));
+          for (int j = 0; j < 2; ++j) {
+            if constexpr ((PC & 1) != 0)
+              glds16_asm(p.Y + (size_t)ks * BK * p.Hin + yo[KK][j], lds_addr(dst + po[KK][j]));
+            else
+              glds16_asm(p.dZ + (size_t)ks * BK * p.Hout + zo[KK][j], lds_addr(dst + Cfg::YBYTES + po[KK][j]));
+          }
         }
       };
       auto read2 = [&](auto sg, int slot) {

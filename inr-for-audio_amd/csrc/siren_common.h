@@ -14,6 +14,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_AS __attribute__((address_space(3)))
 
+// LDS-DMA issue of the ping-pong K-loops' staging pieces (two halves 1 KiB apart in LDS; gemm_nt.hip,
+// gemm_tn.hip): 1 = one statement per piece under one M0 value (glds16x2o_asm_s), 0 = one statement per
+// DMA (glds16_asm_s / glds16_asm; measurement builds)
+#ifndef SIREN_GLDS_PAIR
+#define SIREN_GLDS_PAIR 1
+#endif
+
 namespace siren {
 
 constexpr float kInv2Pi = 0.15915494309189535f;  // 1/(2*pi), rounded to fp32
@@ -89,6 +96,27 @@ __device__ __forceinline__ void glds16_asm_s(unsigned voff, const void* sbase, u
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds_byte))
+      : "memory");
+}
+
+// Two LDS-DMAs of one staging piece in one statement (SIREN_GLDS_PAIR): the piece's second half lies
+// 1 KiB further in LDS and `d` bytes further in the operand.  The instruction offset is added to the
+// global AND the LDS address of an LDS-DMA, so both go out under one M0 value: the second takes
+// offset:1024 with the lane offset voff1m = voff0 + d - 1024.  One M0 save / set / restore and one
+// readfirstlane per piece instead of per DMA (round 6: forward -0.5%, dX -0.8%, bit-identical,
+// profiles/r22/ab_glds_*.json).  An M0 stepped by s_add_u32 between the two DMAs instead clobbers SCC,
+// which hipcc may hold live across the statement: the fused last layer's outputs changed (same A/B).
+__device__ __forceinline__ void glds16x2o_asm_s(unsigned voff0, unsigned voff1m, const void* sbase, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %3\n\t"
+      "global_load_lds_dwordx4 %2, %3 offset:1024\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff0), "v"(voff1m), "s"(sbase), "s"(lds_byte)
       : "memory");
 }
 

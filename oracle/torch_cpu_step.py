@@ -29,10 +29,26 @@ class _Sine(nn.Module):
         return torch.sin(self.omega * self.linear(x))
 
 
-def build(in_dim, hidden, n_inner, omega0, omega, seed=0):
+class _Snake(nn.Module):
+    """nn.Linear + Snake (models.py:235-241): x + (1/a) sin^2(a x), trainable a per channel."""
+
+    def __init__(self, fin, fout, a0):
+        super().__init__()
+        self.linear = nn.Linear(fin, fout)
+        self.a = nn.Parameter(torch.ones(fout) * a0)
+
+    def forward(self, x):
+        z = self.linear(x)
+        return z + (1.0 / self.a) * torch.pow(torch.sin(z * self.a), 2)
+
+
+def build(in_dim, hidden, n_inner, omega0, omega, seed=0, n_snake=0, a0=0.5):
+    """First SineLayer, n_inner hidden SineLayers, n_snake Linear + Snake layers, final Linear
+    (models.py:306-394 with first_linear=False, num_tanh=0, last_linear=True)."""
     torch.manual_seed(seed)
     layers = [_Sine(in_dim, hidden, omega0, True)]
     layers += [_Sine(hidden, hidden, omega, False) for _ in range(n_inner)]
+    layers += [_Snake(hidden, hidden, a0) for _ in range(n_snake)]
     last = nn.Linear(hidden, 1)
     with torch.no_grad():
         lim = math.sqrt(6 / hidden) / omega
@@ -42,11 +58,11 @@ def build(in_dim, hidden, n_inner, omega0, omega, seed=0):
 
 
 def time_steps(n_coords=65536, hidden=1024, n_inner=4, steps=6, threads=None, omega0=3000.0,
-               omega=30.0, seed=0, in_dim=1):
+               omega=30.0, seed=0, in_dim=1, n_snake=0, a0=0.5):
     """Median wall time of steps 2..k of the full-batch loop (BASELINE.md CPU plan)."""
     if threads:
         torch.set_num_threads(int(threads))
-    model = build(in_dim, hidden, n_inner, omega0, omega, seed)
+    model = build(in_dim, hidden, n_inner, omega0, omega, seed, n_snake=n_snake, a0=a0)
     t = torch.linspace(-1, 1, n_coords).reshape(1, n_coords, 1)
     y = 0.5 * torch.sin(37 * t) + 0.3 * torch.sin(91 * t + 0.5)
     if in_dim == 2:  # (t, ch) rows: channel -1 / +1 alternating

@@ -130,6 +130,47 @@ def test_inner_fwd_act(lib, dev, tile, act, R, H, amag, head):
         assert np.max(np.abs(got - ref)) < 1e-4 * max(1.0, np.max(np.abs(ref)))
 
 
+@pytest.mark.parametrize("act", [SNAKE, TANH])
+@pytest.mark.parametrize("H", [256, 512])
+def test_inner_fwd_act_lines_queue(lib, dev, act, H):
+    """The whole-line Snake / Tanh forward (ACTL, taken at K <= 512) on the dynamic tile queue: 16-32
+    tiles of 256 x 256 give a grid that is a multiple of 8, so the queue kernel runs (the
+    R = 512 cases above have <= 4 tiles and only ever reach the static walk).  Its outputs must equal
+    the static walk's bit for bit and lie within one fp16 rounding of fp64."""
+    R = 4096
+    rng = np.random.default_rng(33)
+    X, W, b = _inputs(rng, R, H)
+    a = (0.5 * rng.uniform(0.5, 1.5, H)).astype(F32)
+    Xd, Wd, bd, ad = to_dev(X, dev, H16), to_dev(W, dev, H16), to_dev(b, dev), to_dev(a, dev)
+    outs = []
+    ok(lib.siren_set_option(0, 256), lib)
+    try:
+        for queue in (1, 0):
+            ok(lib.siren_set_option(8, queue), lib)
+            Y, C, E = (torch.full((R, H), float("nan"), dtype=H16, device=dev) for _ in range(3))
+            ok(lib.siren_inner_fwd_act(ptr(Xd), ptr(Wd), ptr(bd), act, ctypes.c_float(1.0), ptr(ad), R, H, ptr(Y),
+                                       ptr(C), ptr(E), None, None, ptr(new_tileq(dev)), S()), lib)
+            torch.cuda.synchronize()
+            outs.append((Y, C, E) if act == SNAKE else (Y, C))
+    finally:
+        lib.siren_set_option(8, 1)
+        lib.siren_set_option(0, 0)
+    for q, s in zip(*outs):
+        assert torch.equal(q, s)
+    z = X.astype(np.float64) @ W.astype(np.float64).T + b
+    slack = 8e-6
+    Y, C = outs[0][0], outs[0][1]
+    if act == SNAKE:
+        y, d, e = _snake_ref(z, a.astype(np.float64))
+        assert within_f16(f16_np(Y), y, slack) <= 0
+        assert within_f16(f16_np(C), d, 2 * slack) <= 0
+        assert within_f16(f16_np(outs[0][2]), e, 2 * slack * (np.max(np.abs(z)) + 1) / float(a.min())) <= 0
+    else:
+        y = np.tanh(z)
+        assert within_f16(f16_np(Y), y, 1e-6) <= 0
+        assert within_f16(f16_np(C), 1.0 - y * y, 2e-6) <= 0
+
+
 def test_snake_small_az_error(lib, dev):
     """The Snake epilogue's double angle (siren_common.h snake_epi: sin^2(az) = (1 - cos 2az)/2) cancels
     for small |az|: t = sin^2(az)/a carries the absolute error of the hardware cos near 1 (~2^-24)

@@ -228,9 +228,25 @@ def test_bench_kernel_kinds_cover_every_template_form():
     want = {"0, false": "inner_fwd", "0, false, true": "inner_fwd", "0, false, false": "inner_fwd",
             "1, false": "bwd_dx", "1, false, false": "bwd_dx", "1, false, true": "bwd_dx",
             "2, false, false": "bwd_dx0", "7, true, false": "head_fwd", "7, true": "head_fwd",
-            "3, false, false": None}
+            "3, false, false": None, "3, false, true, true": None, "0, false, true, false": "inner_fwd"}
     for args, kind in want.items():
         hits = [k for k in bench.KIND_MATCH if bench.kind_match(k, cfg.format(args))]
         assert hits == ([kind] if kind else []), (args, hits)
     tn = "void siren::gemm_tn_kernel<siren::TnCfg<256, 256, 2, 4, 64, 2, 2> >(siren::TnParams)"
     assert [k for k in bench.KIND_MATCH if bench.kind_match(k, tn)] == ["bwd_dw"]
+
+
+def test_bench_bytes_per_row_live_stack():
+    """bench.py's HBM byte model for the width-256 Snake stacks (--config live / default): per row, fp16
+    activations (2 B), the last hidden layer fused with the head."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    e = 2 * 256
+    live = bench.siren_bytes_per_row(["snake"] * 4, 256)
+    assert live == {"first_fwd": 4 + 2 * e, "inner_fwd": 3 * 4 * e, "head_fwd": 2 * e, "bwd_dx": 3 * 4 * e,
+                    "bwd_dx0": 2 * e, "bwd_dw": 4 * 2 * e}
+    dflt = bench.siren_bytes_per_row(["sine", "sine", "snake", "snake"], 256)
+    # forwards: sine 3e, sine 3e, snake 4e; dX into snake (i=3), sine (2), sine (1): 4e + 3e + 3e
+    assert dflt["inner_fwd"] == 10 * e and dflt["bwd_dx"] == 10 * e and dflt["bwd_dw"] == 8 * e
+    assert bench.STACKS["live"] == (0, 4) and bench.CONFIGS["live"][0] == 256 and bench.CONFIGS["live"][3] == 441_000

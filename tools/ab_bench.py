@@ -72,7 +72,8 @@ def main():
     gs = torch.tensor([2.0 ** 9, 2.0 ** -9], device=dev)
     tq = _lib.new_tileq(dev)
     splits = list(libs.values())[0].siren_default_splits(R, H)
-    slab = torch.empty(int(list(libs.values())[0].siren_slab_floats(H, splits)), device=dev)
+    for nm in libs:  # the dW split-K slab, per library so that the parity check covers dW too
+        outs[nm]["slab"] = torch.zeros(int(list(libs.values())[0].siren_slab_floats(H, splits)), device=dev)
     flops = 2.0 * R * H * H
 
     def case(nm, lib, kind, onm=None):
@@ -103,7 +104,7 @@ def main():
             return lambda: lib.siren_inner_fwd_act(P(X), P(W), P(b), act, ctypes.c_float(1.0), P(a_snake), R, H,
                                                    P(o["Y"]), P(o["C"]), P(o["E"]), None, None, P(tq), s())
         if kind == "dw":
-            return lambda: lib.siren_inner_bwd_dw(P(X), P(dZ), R, H, splits, 0, P(slab), s())
+            return lambda: lib.siren_inner_bwd_dw(P(X), P(dZ), R, H, splits, 0, P(o["slab"]), s())
         raise ValueError(kind)
 
     kinds = args.only.split(",")
@@ -115,8 +116,6 @@ def main():
 
     def parity(tag):
         for k in kinds:
-            if k == "dw":
-                continue
             got = {}
             for nm in libs:
                 for t_ in outs[nm].values():
@@ -127,7 +126,8 @@ def main():
                 got[nm] = {"fwd": (o["Y"], o["C"]), "fwd_head": (o["Y"], o["C"], o["hp"]), "dx": (o["dZp"], o["part"]),
                            "dx_snake": (o["dZp"], o["part"]), "dx_tanh": (o["dZp"], o["part"]),
                            "fwd_snake": (o["Y"], o["C"], o["E"]), "fwd_tanh": (o["Y"], o["C"]),
-                           "dx0": (o["part"],), "fwd_hb": (o["out"], o["g"], o["sse"], o["dZp"], o["part"])}[k]
+                           "dx0": (o["part"],), "fwd_hb": (o["out"], o["g"], o["sse"], o["dZp"], o["part"]),
+                           "dw": (o["slab"],)}[k]
                 got[nm] = tuple(x.clone() for x in got[nm])
             for nm in libs:
                 if nm != base:

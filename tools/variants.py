@@ -340,7 +340,36 @@ VARIANTS["ffnt"] = {"elementwise.hip": [
      "    if constexpr (STORE_C) __builtin_nontemporal_store(cv, (h16x8*)(C0 + m * ld + n));")]}
 
 
+# LDS-DMA issue one statement per DMA (siren_common.h SIREN_GLDS_PAIR 0: the round-5 issue path; the
+# product issues a staging piece's two DMAs under one M0 value)
+VARIANTS["glds0"] = {}
+DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",)}
+
+# tools/pending/dx_snake_lines.patch: whole-line dZ stores in the dX into a Snake layer at K <= 512
+VARIANTS["dxsl"] = {"gemm_nt.hip": [
+    ("(ACTL && MODE == NT_FWD_TANH && !HEAD));", "(ACTL && (MODE == NT_FWD_TANH || MODE == NT_DX_SNAKE) && !HEAD));"),
+    ("""      auto piece = [&](auto jc, auto ppc, const uint4& cpv, const uint4& epv) {""",
+     """      uint4 dzrow[SN / 2];  // NT_DX_SNAKE with whole-line stores (Lay::LINES): a row piece's two 16-B pieces
+      auto piece = [&](auto jc, auto ppc, const uint4& cpv, const uint4& epv) {"""),
+    ("""        if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE)
+          st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+      };""",
+     """        if constexpr (MODE == NT_DX_SNAKE && Lay::LINES) {
+          dzrow[pp] = swap16_pair(dzp[0], dzp[1]);
+          if constexpr (pp == SN / 2 - 1) lines_out(p.dZ, mrow0 + j * 16, n0 + wn * TN, dzrow);
+        } else if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE) {
+          st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+        }
+      };"""),
+    ("""    case NT_DX_SNAKE: return launch_nt<Cfg, NT_DX_SNAKE, false>(p, s, persistent);""",
+     """    case NT_DX_SNAKE:
+      return (Cfg::PP && p.K <= 512) ? launch_nt<Cfg, NT_DX_SNAKE, false, true>(p, s, persistent)
+                                     : launch_nt<Cfg, NT_DX_SNAKE, false>(p, s, persistent);"""),
+]}
+
+
 def build(name: str, extra_defines=()) -> str:
+    extra_defines = (*DEFINES.get(name, ()), *extra_defines)
     patches = VARIANTS[name]
     out = os.path.join(ROOT, "inr-for-audio_amd", f"libsiren_{name}.so")
     with tempfile.TemporaryDirectory() as tmp:
