@@ -445,7 +445,7 @@ enum siren_prof_kind {
  * SIREN_OPT_HB_FAULT = measurement / test hook of the fused last layer's hand-off, accepted only by
  *   -DSIREN_DIAG libraries (product: SIREN_ERR_CONFIG for non-zero): bit 0 -- the blocks of column
  *   tile 1 never publish their head partials; value >> 8 (when non-zero) -- the wait's poll limit
- *   (default 2^25 polls of s_sleep 1).  Used to drive the timeout branch in tests.
+ *   (default 2^23 polls of s_sleep 1, ~1.3 s).  Used to drive the timeout branch in tests.
  * SIREN_OPT_HEAD_FUSE = 1 (default): siren_train_step runs a sine last layer on 256x256
  * ping-pong tiles as one launch with the head, the loss gradient and the head backward
  * (dZ_L is written instead of Y_L / C_L; the backward scale S then comes from a bound of

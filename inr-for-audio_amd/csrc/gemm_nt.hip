@@ -178,11 +178,13 @@ __device__ __forceinline__ float tanh_epi(float x) {
 
 // NT_FWD_HB: head_part word not yet published by its column tile's block (launch_nt fills it)
 constexpr unsigned kHeadPending = 0xFFFFFFFFu;
-// polls (s_sleep 1 = 64 clocks each, ~1-1.4 s in all) before a hand-off wait gives up; a partner
-// normally publishes within one tile period (~40 us).  A wait that gives up is counted in the
-// range guard's stall word (NtParams::stall -> GuardState::stalls), which voids the step: the
-// update kernels skip it and the engine raises (include/siren_hip.h siren_guard)
-constexpr int kHeadSpinLimit = 1 << 25;
+// polls before a hand-off wait gives up: a poll (an agent-scope load and s_sleep 1) takes 0.16 us
+// (measured, tools/handoff_timeout.py: 5.4 s at 2^25 polls, profiles/r22/handoff_timeout.json), so
+// 2^23 polls are ~1.3 s, against a partner that normally publishes within one tile period (~40 us).
+// A wait that gives up is counted in the range guard's stall word (NtParams::stall ->
+// GuardState::stalls), which voids the step: the update kernels skip it and the engine raises
+// (include/siren_hip.h siren_guard); every other wait of the step then stops within kStallCheck polls
+constexpr int kHeadSpinLimit = 1 << 23;
 // a waiting thread re-reads the stall word every kStallCheck polls (power of two)
 constexpr int kStallCheck = 256;
 

@@ -18,6 +18,7 @@ import time
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEFAULT_LIMIT = 1 << 23  # gemm_nt.hip kHeadSpinLimit (2^25 until round 6: 5.4 s per voided launch)
 sys.path.insert(0, ROOT)
 
 
@@ -57,7 +58,7 @@ def main():
             assert diag.siren_set_option(10, 0) == 0
         stalls = int(eng.guard[5].item())
         eng.clear_stalls()
-        polls = lim if lim > 0 else 1 << 25
+        polls = lim if lim > 0 else DEFAULT_LIMIT
         out["runs"].append({"limit": lim or "default", "polls": polls, "step_s": round(dt, 4), "stalls": stalls,
                             "us_per_poll": round((dt - clean) / polls * 1e6, 4)})
         print(json.dumps(out["runs"][-1]), flush=True)

@@ -1,7 +1,9 @@
 #!/usr/bin/env bash
 # Round profile on the GPU box (run through gpurun from the repo root):
 #   bench.json              the default bench line (incl. cpu_baseline)
-#   trace/                  rocprofv3 --kernel-trace --stats of a short bench run
+#   trace/                  rocprofv3 --kernel-trace --stats of a bench run (20 steps after 5 warm-up)
+#   kernel_trace_medians.json, frac_summary.json  per-GEMM mean / median launch, fractions by events,
+#                           rocprof mean and median, and the clock each ran at (GRBM_GUI_ACTIVE)
 #   bench_pmc_hbm.json      FETCH_SIZE and WRITE_SIZE, each in its own --pmc pass
 #   bench_pmc_mfma.json     SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE: MFMA utilisation per kernel
 #   bench_pmc_lds.json      SQ_LDS_IDX_ACTIVE / _BANK_CONFLICT / _UNALIGNED_STALL + GRBM_GUI_ACTIVE
@@ -19,7 +21,7 @@ cd /tmp && export TMPDIR=/tmp
 python3 "$ROOT/__graft_entry__.py"
 timeout -k 10 400 python3 "$ROOT/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-recon-snr > "$OUT/trace.log" 2>&1 &&
+  python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-recon-snr > "$OUT/trace.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
   python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-recon-snr > "$OUT/pmc_fetch.log" 2>&1 &&
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
@@ -36,6 +38,8 @@ python3 "$ROOT/tools/pmc_attr.py" "$OUT/fwd_dx_pmc_attribution.json" "$OUT/attr_
 python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_lds.json" "$OUT/pmc_lds" &&
 python3 "$ROOT/tools/pmc_summary.py" "$OUT/bench_pmc_hbm.json" "$OUT/pmc_fetch" "$OUT/pmc_write" &&
 python3 "$ROOT/tools/pmc_mfma.py" "$OUT/bench_pmc_mfma.json" "$OUT/pmc_mfma" &&
+python3 "$ROOT/tools/trace_medians.py" "$(ls "$OUT"/trace/*kernel_trace.csv | head -n 1)" "$OUT/bench.json" "$OUT/kernel_trace_medians.json" &&
+python3 "$ROOT/tools/frac_summary.py" "$OUT" &&
 for c in cfg3 cfg4 cfg5; do
   # every config line carries its CPU baseline (cfg3 / cfg4: the SIREN port at the job's thread share)
   timeout -k 10 300 python3 "$ROOT/bench.py" --config $c > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" &&

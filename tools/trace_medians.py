@@ -32,7 +32,7 @@ def main(trace: str, bench: str, out: str) -> None:
                "min_ms": min(v)} for k, v in durs.items() if v}
     line = json.loads(open(bench).read().strip().splitlines()[-1])
     res["bench_events_inner_fwd_avg_ms"] = line["kernels"]["inner_fwd"]["avg_ms"]
-    res["note"] = ("rocprofv3 --kernel-trace of bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-recon-snr "
+    res["note"] = ("rocprofv3 --kernel-trace of bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-recon-snr "
                    "(tools/profile_round.sh); the mean includes the warm-up steps' first launches, the median "
                    "is the steady state")
     json.dump(res, open(out, "w"), indent=1)
