@@ -451,6 +451,11 @@ def main():
     ap.add_argument("--no-recon-snr", action="store_true", help="skip the recon-SNR fit (cfg2, N = 1)")
     ap.add_argument("--cpu-coords", type=int, default=65536)
     ap.add_argument("--cpu-steps", type=int, default=6)
+    ap.add_argument("--set-option", action="append", default=[], metavar="K=V",
+                    help="measurement only: siren_set_option(K, V) before the engine is built (e.g. 9=0: the last "
+                         "layer unfused); the line lists them in config.options")
+    ap.add_argument("--lib", default=None, help="measurement only: time another build of the library (a variant "
+                    "from tools/variants.py), checked for its ABI; the line then names it in config.lib")
     args = ap.parse_args()
 
     import __graft_entry__ as ge
@@ -470,7 +475,10 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(dev)
         dist.init_process_group(args.backend)
-    lib = _lib.load()
+    lib = _lib.load(os.path.join(ROOT, args.lib)) if args.lib else _lib.load()
+    for kv in args.set_option:
+        k, v = (int(x) for x in kv.split("="))
+        _lib.check(lib.siren_set_option(k, v), f"siren_set_option({k}, {v})")
     ranks = world
     if args.emulate_ranks:
         if world != 1 or args.config not in ("cfg2", "live", "default"):
@@ -587,7 +595,8 @@ def main():
                    "name": args.config, "global_batch": n_total, "coords_per_gpu": per_gpu, "hidden": H,
                    "layers": layers, "in_features": in_dim, "omega0": omega0, "hidden_omega": 30.0,
                    "micro_batches_per_gpu": eng.n_micro, "parallelism": f"dp{world}",
-                   "backend": args.backend if world > 1 else None},
+                   "backend": args.backend if world > 1 else None, "lib": args.lib,
+                   "options": args.set_option or None},
         "roofline": {"bound": "mfma", "kernel": dom,
                      "kernel_choice": "pinned: the SineLayer forward GEMM (north_star's inner GEMM), "
                                       "timed with HIP events over the timed region",

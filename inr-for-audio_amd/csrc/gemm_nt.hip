@@ -309,12 +309,17 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // scratch, 16-B chunks XOR-swizzled by row (conflict-free both ways), and each store writes rows
   // 8q .. 8q+7 as 8 lanes x 16 B per row.  Same bytes and store count as 16 rows x 64 B, but no
   // half-line writes.  Same-wave LDS accesses complete in order, so the reads see this
-  // wave's writes and the next output's writes follow the reads.  row = this lane's row, col = the
-  // wave's first column.
+  // wave's writes and the next output's writes follow the reads.  row = the piece's first row and
+  // col = the wave's first column, both wave-uniform: each store is then a wave-uniform 64-bit base in
+  // SGPRs plus a 32-bit lane offset that is the same for every piece (the saddr form), where per-lane
+  // 64-bit addresses cost 10 64-bit VALU per row piece (v_mad_i64_i32, v_lshl_add_u64; gfx950 listing)
   auto lines_out = [&](h16* out, int row, int col, const uint4 (&v)[Cfg::SN / 2]) {
     static_assert(Cfg::SN == 4, "a wave's row piece is one 128-B line");
     const int pr = lane & 15, pc = swap16_col(lane) >> 3;  // this lane's piece: row, 16-B chunk
     const int qr = lane >> 3, qc = lane & 7;                // line layout: row (+ 8 q), chunk
+    const char* ub = (const char*)(out + (size_t)row * LD + col);
+    unsigned lo = (unsigned)((qr * LD + qc * 8) * 2);
+    asm("" : "+v"(lo));  // kept 32-bit at the stores (a hoisted 64-bit zext defeats the saddr form)
     if constexpr (Lay::HALF) {
       // rows 8h .. 8h+7 per pass.  No lane may skip a pass's write: the compiler treats the scratch
       // per lane, and a write under a divergent branch was moved past the other lanes' reads (wrong
@@ -324,7 +329,6 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       char* sh = smem + Cfg::RING + wave * 1024;
       char* dm = smem + Lay::DM + lane * 32;
       const int r8 = pr & 7;
-      const size_t hbase = (size_t)(row - pr + qr) * LD + col + qc * 8;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const bool mine = (pr >> 3) == h;
@@ -338,7 +342,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         __builtin_amdgcn_wave_barrier();
         const uint4 line = *(const uint4*)(sh + qr * 128 + ((qc ^ qr) << 4));
         __builtin_amdgcn_wave_barrier();
-        stl(out + hbase + (size_t)(8 * h) * LD, line);
+        unsigned lh = lo;
+        asm("" : "+v"(lh));  // one opaque copy per store: no store's address is derived from another's
+        stl((h16*)(ub + (size_t)(16 * h) * LD + lh), line);
       }
       return;
     }
@@ -349,7 +355,6 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = v[pp];
     }
     __builtin_amdgcn_wave_barrier();  // cross-lane exchange: the reads stay after every lane's writes
-    const size_t fbase = (size_t)(row - pr + qr) * LD + col + qc * 8;
     uint4 line[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -358,7 +363,11 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     }
     __builtin_amdgcn_wave_barrier();  // ... and the next output's writes after these reads
 #pragma unroll
-    for (int q = 0; q < 2; ++q) stl(out + fbase + (size_t)(8 * q) * LD, line[q]);
+    for (int q = 0; q < 2; ++q) {
+      unsigned lq = lo;
+      asm("" : "+v"(lq));  // one opaque copy per store: no store's address is derived from another's
+      stl((h16*)(ub + (size_t)(16 * q) * LD + lq), line[q]);
+    }
   };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
@@ -367,8 +376,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   float* a_lds = (float*)(smem + Lay::A);    // Snake: a
   float* ia_lds = (float*)(smem + Lay::IA);  // Snake: 1/a (the same IEEE quotient the epilogue used per element)
   if constexpr (nt_is_fwd(MODE)) {
+    // the sine modes' bias in revolutions, b * omega / (2 pi), once per block (the same fp32 product the
+    // epilogues formed per tile); 1 for Snake / Tanh
+    const float xb = (MODE == NT_FWD || MODE == NT_FWD_HB) ? p.omega * kInv2Pi : 1.0f;
     for (int c = tid * 4; c < N; c += Cfg::THREADS * 4) {
-      *(float4*)(bias_lds + c) = *(const float4*)(p.bias + c);
+      const float4 b4 = *(const float4*)(p.bias + c);
+      *(float4*)(bias_lds + c) = float4{b4.x * xb, b4.y * xb, b4.z * xb, b4.w * xb};
       if constexpr (HEAD) *(float4*)(hw_lds + c) = *(const float4*)(p.head_w + c);
       if constexpr (nt_is_snake_fwd(MODE)) {
         const float4 a4 = *(const float4*)(p.act_a + c);
@@ -397,34 +410,43 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   constexpr int EB0 = (MODE == NT_DX0_SNAKE) ? SIREN_SNAKE0_EB : SIREN_SNAKE_EB;
   constexpr int EB = EB0 < SM ? EB0 : SM;
   static_assert(SM % EB == 0, "Snake epilogue batches");
+  // Row-piece accesses of the epilogues: a wave-uniform row base (SGPRs) plus a 32-bit lane byte offset kept
+  // 32-bit at the access by an opaque copy, so that hipcc emits the saddr form (one SGPR pair, one VGPR)
+  // instead of per-lane 64-bit address arithmetic (v_mad_i64_i32, v_lshl_add_u64: lines_out)
+  auto at_lane = [](const void* ub, unsigned lo) -> char* {
+    asm("" : "+v"(lo));
+    return (char*)ub + lo;
+  };
+  // this lane's 16-B piece of a row piece (row lane & 15, columns swap16_col(lane) ..): byte offset in [*][LD] fp16
+  const unsigned lane_piece = (unsigned)(((lane & 15) * LD + swap16_col(lane)) * 2);
+  auto rowp = [&](const h16* base, int row_u, int col_u) { return (const char*)(base + (size_t)row_u * LD + col_u); };
   uint4 cp_in[PRE_J > 0 ? PRE_J : 1][SN / 2];
   uint4 ce_in[HAS_E ? EB : 1][2];
   float t_in[SM][2];
   auto pre = [&](int g) {
     int m0, n0;
     tile_of(g, m0, n0);
-    const int npc = n0 + wn * TN + swap16_col(lane);
-    const int mrow0 = m0 + wm * TM + (lane & 15);
+    const int mrowu = m0 + wm * TM, ncu = n0 + wn * TN;  // the wave's first row and column (wave-uniform)
     if constexpr (!nt_is_fwd(MODE)) {
 #pragma unroll
       for (int j = 0; j < PRE_J; ++j)
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp)
-          cp_in[j][pp] = *(const uint4*)(p.Cprev + (size_t)(mrow0 + j * 16) * LD + npc + pp * 32);
+          cp_in[j][pp] = *(const uint4*)at_lane(rowp(p.Cprev, mrowu + j * 16, ncu), lane_piece + pp * 64);
       if constexpr (HAS_E) {
 #pragma unroll
         for (int j = 0; j < EB; ++j) {
-          const size_t off = (size_t)(mrow0 + j * 16) * LD + npc;
-          ce_in[j][0] = *(const uint4*)(p.Cprev + off);
-          ce_in[j][1] = *(const uint4*)(p.Eprev + off);
+          ce_in[j][0] = *(const uint4*)at_lane(rowp(p.Cprev, mrowu + j * 16, ncu), lane_piece);
+          ce_in[j][1] = *(const uint4*)at_lane(rowp(p.Eprev, mrowu + j * 16, ncu), lane_piece);
         }
       }
       if constexpr (nt_is_dx0(MODE)) {
 #pragma unroll
         for (int j = 0; j < SM; ++j) {
-          const size_t m = mrow0 + j * 16;
-          t_in[j][0] = p.t[m * p.in_dim];
-          t_in[j][1] = (p.in_dim > 1) ? p.t[m * p.in_dim + 1] : 0.f;
+          const float* tb = p.t + (size_t)(mrowu + j * 16) * p.in_dim;
+          const unsigned lt = (unsigned)((lane & 15) * p.in_dim * 4);
+          t_in[j][0] = *(const float*)at_lane(tb, lt);
+          t_in[j][1] = (p.in_dim > 1) ? *(const float*)at_lane(tb, lt + 4) : 0.f;
         }
       }
     }
@@ -434,7 +456,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     tile_of(g, m0, n0);
     const int tm = m0 / BM, tn = n0 / BN;
     const int npc = n0 + wn * TN + swap16_col(lane);      // swapped layout: this lane's piece
-    const int mrow0 = m0 + wm * TM + (lane & 15);
+    const int mrowu = m0 + wm * TM;                       // the wave's first row (wave-uniform)
+    const int mrow0 = mrowu + (lane & 15);
 
     if constexpr (nt_is_hb(MODE)) {
       // The last hidden layer fused with the head, the loss gradient and the head backward, for
@@ -448,11 +471,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       constexpr bool SNK = MODE == NT_FWD_HB_SNAKE, TNH = MODE == NT_FWD_HB_TANH;
       const int nq = n0 + wn * TN + 4 * (lane >> 4);
       const float xs = (MODE == NT_FWD_HB) ? p.omega * kInv2Pi : 1.0f;
-      float4 bias[SN], hw[SN];
+      float4 bias[SN], hw[SN];  // (bias_lds holds b * xs)
 #pragma unroll
       for (int i = 0; i < SN; ++i) {
-        const float4 b = *(const float4*)(bias_lds + nq + i * 16);
-        bias[i] = float4{b.x * xs, b.y * xs, b.z * xs, b.w * xs};
+        bias[i] = *(const float4*)(bias_lds + nq + i * 16);
         hw[i] = *(const float4*)(hw_lds + nq + i * 16);
       }
       float hp[SM];
@@ -506,7 +528,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             }
             hp[j] += sv[0] * hw[i].x + sv[1] * hw[i].y + sv[2] * hw[i].z + sv[3] * hw[i].w;
           }
-          if constexpr (SNK) st16(p.E + (size_t)(mrow0 + j * 16) * LD + npc + pp * 32, swap16_pair(epair[0], epair[1]));
+          if constexpr (SNK)
+            st16((h16*)at_lane(rowp(p.E, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(epair[0], epair[1]));
         }
       }
 #pragma unroll
@@ -631,7 +654,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         if constexpr (SNK) {
 #pragma unroll
           for (int pp = 0; pp < SN / 2; ++pp)
-            eall[j][pp] = *(const uint4*)(p.E + (size_t)(mrow0 + j * 16) * LD + npc + pp * 32);
+            eall[j][pp] = *(const uint4*)at_lane(rowp(p.E, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64);
         }
         uint4 dzq[SN / 2];  // whole-line stores (Lay::LINES): this row piece's two 16-B pieces
 #pragma unroll
@@ -661,9 +684,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
           }
           if constexpr (Lay::LINES) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
-          else st16(p.dZ + (size_t)(mrow0 + j * 16) * LD + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+          else st16((h16*)at_lane(rowp(p.dZ, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(dzp[0], dzp[1]));
         }
-        if constexpr (Lay::LINES) lines_out(p.dZ, mrow0 + j * 16, n0 + wn * TN, dzq);
+        if constexpr (Lay::LINES) lines_out(p.dZ, mrowu + j * 16, n0 + wn * TN, dzq);
       }
 #pragma unroll
       for (int pp = 0; pp < SN / 2; ++pp)
@@ -732,11 +755,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
     } else if constexpr (nt_is_fwd(MODE)) {
       const int nq = n0 + wn * TN + 4 * (lane >> 4);     // natural layout: this lane's columns
       const float xs = (MODE == NT_FWD) ? p.omega * kInv2Pi : 1.0f;
-      float4 bias[SN], hw[SN];
+      float4 bias[SN], hw[SN];  // (bias_lds holds b * xs)
 #pragma unroll
       for (int i = 0; i < SN; ++i) {
-        const float4 b = *(const float4*)(bias_lds + nq + i * 16);
-        bias[i] = float4{b.x * xs, b.y * xs, b.z * xs, b.w * xs};
+        bias[i] = *(const float4*)(bias_lds + nq + i * 16);
         if constexpr (HEAD) hw[i] = *(const float4*)(hw_lds + nq + i * 16);
       }
       float hp[SM];
@@ -804,13 +826,14 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         if constexpr (Lay::LINES || Lay::HALF) {
           // whole-line stores (lines_out): forward -4.6%, cfg4 -6.5% (static walk,
           // profiles/r19/ab_full_lines.json)
-          lines_out(p.Y, mrow0 + j * 16, n0 + wn * TN, yp);
-          lines_out(p.C, mrow0 + j * 16, n0 + wn * TN, cpk);
-          if constexpr (MODE == NT_FWD_SNAKE) lines_out(p.E, mrow0 + j * 16, n0 + wn * TN, epk);
+          lines_out(p.Y, mrowu + j * 16, n0 + wn * TN, yp);
+          lines_out(p.C, mrowu + j * 16, n0 + wn * TN, cpk);
+          if constexpr (MODE == NT_FWD_SNAKE) lines_out(p.E, mrowu + j * 16, n0 + wn * TN, epk);
           continue;
         }
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
+          // (per-lane addresses here: the head forward has no registers for at_lane's copies -- Snake spilled)
           st16(p.Y + rowoff + npc + pp * 32, yp[pp]);
           st16(p.C + rowoff + npc + pp * 32, cpk[pp]);
           if constexpr (MODE == NT_FWD_SNAKE) st16(p.E + rowoff + npc + pp * 32, epk[pp]);
@@ -907,9 +930,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         }
         if constexpr (MODE == NT_DX_SNAKE && Lay::LINES) {
           dzrow[pp] = swap16_pair(dzp[0], dzp[1]);
-          if constexpr (pp == SN / 2 - 1) lines_out(p.dZ, mrow0 + j * 16, n0 + wn * TN, dzrow);
+          if constexpr (pp == SN / 2 - 1) lines_out(p.dZ, mrowu + j * 16, n0 + wn * TN, dzrow);
         } else if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE) {
-          st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+          st16((h16*)at_lane(rowp(p.dZ, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(dzp[0], dzp[1]));
         }
       };
       if constexpr (HAS_E) {
@@ -930,9 +953,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                 cq[bf][jj][pp] = ce_in[jj][0];
                 eq[bf][jj][pp] = ce_in[jj][1];
               } else {
-                const size_t off = (size_t)(mrow0 + (bq * EB + jj) * 16) * LD + npc + pp * 32;
-                cq[bf][jj][pp] = *(const uint4*)(p.Cprev + off);
-                eq[bf][jj][pp] = *(const uint4*)(p.Eprev + off);
+                const int ru = mrowu + (bq * EB + jj) * 16;
+                cq[bf][jj][pp] = *(const uint4*)at_lane(rowp(p.Cprev, ru, n0 + wn * TN), lane_piece + pp * 64);
+                eq[bf][jj][pp] = *(const uint4*)at_lane(rowp(p.Eprev, ru, n0 + wn * TN), lane_piece + pp * 64);
               }
             }
         };
@@ -964,7 +987,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int pp = 0; pp < SN / 2; ++pp) {
             uint2 cpu[2];
             const uint4 cpv =
-                (j < PRE_J) ? cp_in[j < PRE_J ? j : 0][pp] : *(const uint4*)(p.Cprev + rowoff + npc + pp * 32);
+                (j < PRE_J) ? cp_in[j < PRE_J ? j : 0][pp]
+                            : *(const uint4*)at_lane(rowp(p.Cprev, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64);
             unswap16_pair(cpv, cpu[0], cpu[1]);
             uint2 dzp[2];
 #pragma unroll
@@ -984,9 +1008,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
             }
             if constexpr (Lay::LINES && MODE == NT_DX) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
-            else if constexpr (MODE == NT_DX) st16(p.dZ + rowoff + npc + pp * 32, swap16_pair(dzp[0], dzp[1]));
+            else if constexpr (MODE == NT_DX)
+              st16((h16*)at_lane(rowp(p.dZ, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(dzp[0], dzp[1]));
           }
-          if constexpr (Lay::LINES && MODE == NT_DX) lines_out(p.dZ, mrow0 + j * 16, n0 + wn * TN, dzq);
+          if constexpr (Lay::LINES && MODE == NT_DX) lines_out(p.dZ, mrowu + j * 16, n0 + wn * TN, dzq);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {

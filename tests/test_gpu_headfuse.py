@@ -271,3 +271,55 @@ def test_handoff_timeout_voids_the_step(dev, monkeypatch, cfg):
     assert eng.steps_applied() == 3
     assert bool(torch.isfinite(eng.params).all()) and not torch.equal(eng.params, before[0])
     log(f"handoff_timeout[{cfg}]", stalls=g[5])
+
+
+def test_handoff_timeout_fails_fast(dev, monkeypatch):
+    """Once one hand-off wait of a step has given up, every other wait of the step stops within
+    kStallCheck (256) polls instead of spending its own whole limit: with the
+    fault hook on and a 2^20-poll limit (~0.17 s per wait, tools/handoff_timeout.py), a step of 4
+    micro-batches whose blocks each walk 4 bands per launch would otherwise wait 16 limits in a
+    row (~2.7 s); it must come in under 4 limits.  The step is voided as in the test above."""
+    import time
+    import __graft_entry__ as ge
+    from inr_for_audio_amd import _lib
+    diag = _lib.bind(ge.DIAG_LIB, expect_build_id=_lib.expected_build_id(ge.DIAG_DEFINES))
+    monkeypatch.setattr(_lib, "_lib", diag)
+    from inr_for_audio_amd.engine import SirenEngine
+    from inr_for_audio_amd.models import SirenWithSnakeTanh
+    torch.manual_seed(0)
+    n = 4 * 16384  # 4 micro-batches of 64 bands x 4 column tiles
+    model = SirenWithSnakeTanh(1, 1, 1024, 2, 0, 0, first_omega_0=3000.0, hidden_omega_0=30.0)
+    t = torch.linspace(-1, 1, n).reshape(n, 1)
+    eng = SirenEngine(model, t, 0.5 * torch.sin(37 * t), micro_batch=16384, device=dev)
+    assert eng.lib is diag and eng.n_micro == 4
+    assert diag.siren_set_option(0, 256) == 0  # 256 x 256 tiles at 16 384 rows (the fused path's tile)
+    assert diag.siren_set_option(4, 16) == 0  # 16 blocks: each walks 16 band tiles per launch
+    try:
+        eng.step()
+        torch.cuda.synchronize()
+        fused = diag.siren_profile_enable(64 * eng.n_micro) == 0
+        t0 = time.perf_counter()
+        eng.step()
+        torch.cuda.synchronize()
+        clean = time.perf_counter() - t0
+        prof = _lib.profile_read()
+        diag.siren_profile_enable(0)
+        assert fused and prof["head_fwd"][1] == eng.n_micro, prof  # the fused last layer runs per micro-batch
+        limit = 1 << 20
+        assert diag.siren_set_option(10, (limit << 8) | 1) == 0
+        try:
+            t0 = time.perf_counter()
+            eng.step()
+            torch.cuda.synchronize()
+            voided = time.perf_counter() - t0
+        finally:
+            assert diag.siren_set_option(10, 0) == 0
+    finally:
+        diag.siren_set_option(4, 0)
+        diag.siren_set_option(0, 0)
+    per_limit = limit * 0.16e-6
+    with pytest.raises(_lib.SirenError, match="hand-off"):
+        eng.steps_applied()
+    log("handoff_fail_fast", clean_s=clean, voided_s=voided, per_limit_s=per_limit)
+    assert voided < clean + 4 * per_limit, (voided, per_limit)
+    eng.clear_stalls()

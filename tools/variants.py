@@ -343,7 +343,9 @@ VARIANTS["ffnt"] = {"elementwise.hip": [
 # LDS-DMA issue one statement per DMA (siren_common.h SIREN_GLDS_PAIR 0: the round-5 issue path; the
 # product issues a staging piece's two DMAs under one M0 value)
 VARIANTS["glds0"] = {}
-DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",)}
+# plain (write-back) whole-line epilogue stores instead of non-temporal ones (gemm_nt.hip SIREN_NT_STNT)
+VARIANTS["stnt0"] = {}
+DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",), "stnt0": ("SIREN_NT_STNT=0",)}
 
 # tools/pending/dx_snake_lines.patch: whole-line dZ stores in the dX into a Snake layer at K <= 512
 VARIANTS["dxsl"] = {"gemm_nt.hip": [
