@@ -61,6 +61,11 @@
 #ifndef SIREN_NT_STNT
 #define SIREN_NT_STNT 1
 #endif
+// lines_out: 0 = each lane's MFMA-layout 8-B halves straight into the line scratch; 1 = paired into 16-B row
+// pieces by v_permlane16_swap first (round 5; measurement builds)
+#ifndef SIREN_LINES_SWAP
+#define SIREN_LINES_SWAP 0
+#endif
 
 #ifdef SIREN_DIAG
 #define SIREN_DIAG_ON 1
@@ -313,10 +318,20 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // col = the wave's first column, both wave-uniform: each store is then a wave-uniform 64-bit base in
   // SGPRs plus a 32-bit lane offset that is the same for every piece (the saddr form), where per-lane
   // 64-bit addresses cost 10 64-bit VALU per row piece (v_mad_i64_i32, v_lshl_add_u64; gfx950 listing)
-  auto lines_out = [&](h16* out, int row, int col, const uint4 (&v)[Cfg::SN / 2]) {
+  // v[i]: this lane's 4 columns of column subtile i in the MFMA layout (row lane & 15, columns 16 i + 4 g ..
+  // + 3, g = lane >> 4), packed fp16: 8 B at byte 32 i + 8 g of the row's line.  Each goes into the scratch as
+  // one 8-B half of its swizzled 16-B chunk 2 i + (g >> 1) (SIREN_LINES_SWAP 1: first paired into 16-B row
+  // pieces across 16-lane groups by v_permlane16_swap, as round 5 did -- 4 VALU per row piece more)
+  auto lines_out = [&](h16* out, int row, int col, const uint2 (&v)[Cfg::SN]) {
     static_assert(Cfg::SN == 4, "a wave's row piece is one 128-B line");
     const int pr = lane & 15, pc = swap16_col(lane) >> 3;  // this lane's piece: row, 16-B chunk
+    const int g = lane >> 4;                                // MFMA layout: 16-lane group
     const int qr = lane >> 3, qc = lane & 7;                // line layout: row (+ 8 q), chunk
+    uint4 vs[SIREN_LINES_SWAP ? Cfg::SN / 2 : 1];
+    if constexpr (SIREN_LINES_SWAP != 0) {
+#pragma unroll
+      for (int pp = 0; pp < Cfg::SN / 2; ++pp) vs[pp] = swap16_pair(v[2 * pp], v[2 * pp + 1]);
+    }
     const char* ub = (const char*)(out + (size_t)row * LD + col);
     unsigned lo = (unsigned)((qr * LD + qc * 8) * 2);
     asm("" : "+v"(lo));  // kept 32-bit at the stores (a hoisted 64-bit zext defeats the saddr form)
@@ -332,10 +347,18 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const bool mine = (pr >> 3) == h;
+        if constexpr (SIREN_LINES_SWAP != 0) {
 #pragma unroll
-        for (int pp = 0; pp < Cfg::SN / 2; ++pp) {
-          const int c = pp * 4 + pc;
-          *(uint4*)(mine ? sh + r8 * 128 + ((c ^ r8) << 4) : dm + pp * 16) = v[pp];
+          for (int pp = 0; pp < Cfg::SN / 2; ++pp) {
+            const int c = pp * 4 + pc;
+            *(uint4*)(mine ? sh + r8 * 128 + ((c ^ r8) << 4) : dm + pp * 16) = vs[pp];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < Cfg::SN; ++i) {
+            const int c = 2 * i + (g >> 1);
+            *(uint2*)(mine ? sh + r8 * 128 + ((c ^ r8) << 4) + ((g & 1) << 3) : dm + i * 8) = v[i];
+          }
         }
         // the exchange is across lanes: no LDS access moves over these (LDS is in order within a
         // wave, so they cost no wait; the ordering no longer rests on how the select is written)
@@ -349,10 +372,18 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       return;
     }
     char* sc = smem + Lay::ST + wave * 2048;
+    if constexpr (SIREN_LINES_SWAP != 0) {
 #pragma unroll
-    for (int pp = 0; pp < Cfg::SN / 2; ++pp) {
-      const int c = pp * 4 + pc;
-      *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = v[pp];
+      for (int pp = 0; pp < Cfg::SN / 2; ++pp) {
+        const int c = pp * 4 + pc;
+        *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = vs[pp];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < Cfg::SN; ++i) {
+        const int c = 2 * i + (g >> 1);
+        *(uint2*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4) + ((g & 1) << 3)) = v[i];
+      }
     }
     __builtin_amdgcn_wave_barrier();  // cross-lane exchange: the reads stay after every lane's writes
     uint4 line[2];
@@ -656,7 +687,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int pp = 0; pp < SN / 2; ++pp)
             eall[j][pp] = *(const uint4*)at_lane(rowp(p.E, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64);
         }
-        uint4 dzq[SN / 2];  // whole-line stores (Lay::LINES): this row piece's two 16-B pieces
+        uint2 dzq[SN];  // whole-line stores (Lay::LINES): this row piece's MFMA-layout halves
 #pragma unroll
         for (int pp = 0; pp < SN / 2; ++pp) {
           uint2 dzp[2];
@@ -683,7 +714,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             });
             dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
           }
-          if constexpr (Lay::LINES) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
+          if constexpr (Lay::LINES) {
+            dzq[2 * pp] = dzp[0];
+            dzq[2 * pp + 1] = dzp[1];
+          }
           else st16((h16*)at_lane(rowp(p.dZ, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(dzp[0], dzp[1]));
         }
         if constexpr (Lay::LINES) lines_out(p.dZ, mrowu + j * 16, n0 + wn * TN, dzq);
@@ -767,7 +801,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
         const size_t rowoff = (size_t)(mrow0 + j * 16) * LD;
-        uint4 yp[SN / 2], cpk[SN / 2], epk[SN / 2];
+        uint4 yp[SN / 2], cpk[SN / 2], epk[SN / 2];  // 16-B row pieces (the per-lane stores)
+        uint2 yh[SN], chh[SN], eh[SN];                // MFMA-layout halves (lines_out)
 #pragma unroll
         for (int q = 0; q < SN / 2; ++q) {
           // ping-pong tiles: the lower row half takes its column pairs in reverse, the order of
@@ -805,30 +840,31 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                 c[r] = 1.0f - y * y;
               }
             }
-            ys[h] = as_u2(pack4(s[0], s[1], s[2], s[3]));
-            cs[h] = as_u2(pack4(c[0], c[1], c[2], c[3]));
-            if constexpr (MODE == NT_FWD_SNAKE) es[h] = as_u2(pack4(e[0], e[1], e[2], e[3]));
+            ys[h] = yh[i] = as_u2(pack4(s[0], s[1], s[2], s[3]));
+            cs[h] = chh[i] = as_u2(pack4(c[0], c[1], c[2], c[3]));
+            if constexpr (MODE == NT_FWD_SNAKE) es[h] = eh[i] = as_u2(pack4(e[0], e[1], e[2], e[3]));
             if constexpr (HEAD)
               hp[j] += s[0] * hw[i].x + s[1] * hw[i].y + s[2] * hw[i].z + s[3] * hw[i].w;
           }
-          yp[pp] = swap16_pair(ys[0], ys[1]);
-          cpk[pp] = swap16_pair(cs[0], cs[1]);
-          if constexpr (MODE == NT_FWD_SNAKE) epk[pp] = swap16_pair(es[0], es[1]);
+          if constexpr (!(Lay::LINES || Lay::HALF)) {
+            yp[pp] = swap16_pair(ys[0], ys[1]);
+            cpk[pp] = swap16_pair(cs[0], cs[1]);
+            if constexpr (MODE == NT_FWD_SNAKE) epk[pp] = swap16_pair(es[0], es[1]);
+          }
         }
         if (SIREN_DIAG_ON && (diag & 2048)) {  // diag bit 11: the epilogue without its stores (timing only)
           unsigned keep = 0;
 #pragma unroll
-          for (int pp = 0; pp < SN / 2; ++pp)
-            keep ^= yp[pp].x ^ yp[pp].y ^ yp[pp].z ^ yp[pp].w ^ cpk[pp].x ^ cpk[pp].y ^ cpk[pp].z ^ cpk[pp].w;
+          for (int i = 0; i < SN; ++i) keep ^= yh[i].x ^ yh[i].y ^ chh[i].x ^ chh[i].y;
           asm volatile("" ::"v"(keep));
           continue;
         }
         if constexpr (Lay::LINES || Lay::HALF) {
           // whole-line stores (lines_out): forward -4.6%, cfg4 -6.5% (static walk,
           // profiles/r19/ab_full_lines.json)
-          lines_out(p.Y, mrowu + j * 16, n0 + wn * TN, yp);
-          lines_out(p.C, mrowu + j * 16, n0 + wn * TN, cpk);
-          if constexpr (MODE == NT_FWD_SNAKE) lines_out(p.E, mrowu + j * 16, n0 + wn * TN, epk);
+          lines_out(p.Y, mrowu + j * 16, n0 + wn * TN, yh);
+          lines_out(p.C, mrowu + j * 16, n0 + wn * TN, chh);
+          if constexpr (MODE == NT_FWD_SNAKE) lines_out(p.E, mrowu + j * 16, n0 + wn * TN, eh);
           continue;
         }
 #pragma unroll
@@ -894,9 +930,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       };
       // the 16-B piece (row subtile j, column pair pp) from its Cprev (and Eprev) piece.  Each column
       // partial sums its rows in order 0 .. SM-1 whatever order the pieces go in
-      // NT_DX_SNAKE with whole-line stores (Lay::LINES): a row piece's two 16-B pieces (the Snake batches
+      // NT_DX_SNAKE with whole-line stores (Lay::LINES): a row piece's MFMA-layout halves (the Snake batches
       // below take both column pairs of a row back to back, pair 1 last)
-      uint4 dzrow[SN / 2];
+      uint2 dzrow[SN];
       auto piece = [&](auto jc, auto ppc, const uint4& cpv, const uint4& epv) {
         constexpr int j = decltype(jc)::value, pp = decltype(ppc)::value;
         const size_t rowoff = (size_t)(mrow0 + j * 16) * LD;
@@ -929,7 +965,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
         }
         if constexpr (MODE == NT_DX_SNAKE && Lay::LINES) {
-          dzrow[pp] = swap16_pair(dzp[0], dzp[1]);
+          dzrow[2 * pp] = dzp[0];
+          dzrow[2 * pp + 1] = dzp[1];
           if constexpr (pp == SN / 2 - 1) lines_out(p.dZ, mrowu + j * 16, n0 + wn * TN, dzrow);
         } else if constexpr (MODE == NT_DX || MODE == NT_DX_SNAKE) {
           st16((h16*)at_lane(rowp(p.dZ, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(dzp[0], dzp[1]));
@@ -982,7 +1019,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             t0 = t_in[j][0];
             t1 = t_in[j][1];
           }
-          uint4 dzq[SN / 2];  // NT_DX with whole-line stores: this row piece's two 16-B pieces
+          uint2 dzq[SN];  // NT_DX with whole-line stores: this row piece's MFMA-layout halves
 #pragma unroll
           for (int pp = 0; pp < SN / 2; ++pp) {
             uint2 cpu[2];
@@ -1007,7 +1044,10 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               });
               dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
             }
-            if constexpr (Lay::LINES && MODE == NT_DX) dzq[pp] = swap16_pair(dzp[0], dzp[1]);
+            if constexpr (Lay::LINES && MODE == NT_DX) {
+              dzq[2 * pp] = dzp[0];
+              dzq[2 * pp + 1] = dzp[1];
+            }
             else if constexpr (MODE == NT_DX)
               st16((h16*)at_lane(rowp(p.dZ, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(dzp[0], dzp[1]));
           }

@@ -345,7 +345,9 @@ VARIANTS["ffnt"] = {"elementwise.hip": [
 VARIANTS["glds0"] = {}
 # plain (write-back) whole-line epilogue stores instead of non-temporal ones (gemm_nt.hip SIREN_NT_STNT)
 VARIANTS["stnt0"] = {}
-DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",), "stnt0": ("SIREN_NT_STNT=0",)}
+# lines_out pairs the MFMA-layout halves into 16-B row pieces by v_permlane16_swap first (gemm_nt.hip SIREN_LINES_SWAP)
+VARIANTS["lswap"] = {}
+DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",), "stnt0": ("SIREN_NT_STNT=0",), "lswap": ("SIREN_LINES_SWAP=1",)}
 
 # tools/pending/dx_snake_lines.patch: whole-line dZ stores in the dX into a Snake layer at K <= 512
 VARIANTS["dxsl"] = {"gemm_nt.hip": [
