@@ -424,6 +424,16 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   }
   // dZ carries the backward storage scale S; the fp32 column partials leave unscaled
   const float inv_scale = (!nt_is_fwd(MODE) && p.gscale) ? p.gscale[1] : 1.0f;
+  // the fused last layer's S, 1/S and head bias, loaded once here: loaded in the epilogue, each
+  // tile's phase 2 waited at vmcnt(0) for them, i.e. for the next tile's stages issued before it
+  float hb_scale[2] = {1.0f, 1.0f}, hb_bias = 0.0f;
+  if constexpr (nt_is_hb(MODE)) {
+    hb_scale[0] = p.gscale[0];
+    hb_scale[1] = p.gscale[1];
+    hb_bias = p.b_head[0];
+    // in VGPRs (3 of the 20 free): as SGPRs they pushed 12 more SGPR spills into VGPR lanes
+    asm volatile("" : "+v"(hb_scale[0]), "+v"(hb_scale[1]), "+v"(hb_bias));
+  }
   // NT_DX / NT_DX0 epilogue operands loaded by `pre` (before the next tile's early prefetch).  The
   // rest are loaded by the epilogue in one batch once earlier pieces are consumed (their
   // accumulators free the registers), so a batch waits once, not once per piece behind the
@@ -538,7 +548,8 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               epair[h] = as_u2(pack4(ev[0], ev[1], ev[2], ev[3]));
               asm volatile("" : "+v"(acc[i][j]));
             } else {
-              float cv[4];
+              float cv[4], xa[4];
+              if constexpr (!TNH) fma4_pk(acc[i][j], xs, bias[i], xa);  // as the plain forward
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 if constexpr (TNH) {
@@ -546,7 +557,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
                   sv[r] = y;
                   cv[r] = 1.0f - y * y;
                 } else {
-                  const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
+                  const float x = __builtin_amdgcn_fractf(xa[r]);
                   sv[r] = __builtin_amdgcn_sinf(x);
                   cv[r] = __builtin_amdgcn_cosf(x);
                 }
@@ -557,7 +568,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
               // hand-off into phase 2, keeping the fp32 arguments live across it: 372 B of spills)
               asm volatile("" : "+v"(acc[i][j]));
             }
-            hp[j] += sv[0] * hw[i].x + sv[1] * hw[i].y + sv[2] * hw[i].z + sv[3] * hw[i].w;
+            hp[j] += dot4_pk(sv, hw[i]);
           }
           if constexpr (SNK)
             st16((h16*)at_lane(rowp(p.E, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(epair[0], epair[1]));
@@ -623,7 +634,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           }
           o += v;
         }
-        o += p.b_head[0];
+        o += hb_bias;
         const float a = p.head_omega * o;
         const float ov = p.head_omega > 0.f ? sinf(a) : o;
         if (m < p.n_valid) {
@@ -661,7 +672,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       // needs no multiply of its own; the column partials sum dz S, g S Y (and g S w E) and leave
       // multiplied by 1/S -- power-of-two scalings commute with every rounding, so dZ_L and the
       // partials are bit for bit those of the unscaled order (head_bwd_kernel's ((g w) C) omega)
-      const float om = (MODE == NT_FWD_HB) ? p.omega : 1.0f, S = p.gscale[0], invS = p.gscale[1];
+      const float om = (MODE == NT_FWD_HB) ? p.omega : 1.0f, S = hb_scale[0], invS = hb_scale[1];
       float gm[SM];
 #pragma unroll
       for (int j = 0; j < SM; ++j) gm[j] = g_lds[wm * TM + j * 16 + (lane & 15)] * S;
@@ -695,24 +706,29 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           for (int h = 0; h < 2; ++h) {
             const int i = 2 * pp + h;
             const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);
-            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
             const uint4 pk = __builtin_bit_cast(uint4, acc[i][j]);
             const uint2 yh = uint2{pk.x, pk.y}, ch = uint2{pk.z, pk.w};
-            float d[4];
+            // head_bwd_kernel's dz, ((g w) C) omega (bit-identical), times S (gm carries it; omega
+            // is exactly 1 for a Snake / Tanh layer).  The fp32 x fp32 products and the db_L sums go
+            // in pairs (v_pk_mul_f32 / v_pk_add_f32: per element the same rounding as the scalar
+            // instruction); the products by an fp16 operand stay v_fma_mix_f32 (no packed form)
+            const f32x2 gw01 = f32x2{gm[j], gm[j]} * f32x2{w4.x, w4.y};
+            const f32x2 gw23 = f32x2{gm[j], gm[j]} * f32x2{w4.z, w4.w};
+            f32x2 d01 = f32x2{mul_mix<0>(gw01.x, ch), mul_mix<1>(gw01.y, ch)};
+            f32x2 d23 = f32x2{mul_mix<2>(gw23.x, ch), mul_mix<3>(gw23.y, ch)};
+            if constexpr (MODE == NT_FWD_HB) {
+              d01 *= f32x2{om, om};
+              d23 *= f32x2{om, om};
+              asm volatile("" : "+v"(d01), "+v"(d23));  // rounded to fp32 before the fp16 store (fp32_first)
+            }
+            const f32x2 c01 = f32x2{cs[pp][0][h][0], cs[pp][0][h][1]} + d01;
+            const f32x2 c23 = f32x2{cs[pp][0][h][2], cs[pp][0][h][3]} + d23;
+            cs[pp][0][h][0] = c01.x; cs[pp][0][h][1] = c01.y; cs[pp][0][h][2] = c23.x; cs[pp][0][h][3] = c23.y;
             static_for<0, 4>([&](auto rc) {
               constexpr int r = decltype(rc)::value;
-              // head_bwd_kernel's dz, ((g w) C) omega (bit-identical), times S (gm carries it; omega
-              // is exactly 1 for a Snake / Tanh layer)
-              float dz = mul_mix<r>(gm[j] * wv[r], ch);
-              if constexpr (MODE == NT_FWD_HB) {
-                dz *= om;
-                asm volatile("" : "+v"(dz));  // rounded to fp32 before the fp16 store (fp32_first)
-              }
-              cs[pp][0][h][r] += dz;
               cs[pp][1][h][r] = fma_mix<r>(gm[j], yh, cs[pp][1][h][r]);
-              d[r] = dz;
             });
-            dzp[h] = as_u2(pack4(d[0], d[1], d[2], d[3]));
+            dzp[h] = as_u2(pack4(d01.x, d01.y, d23.x, d23.y));
           }
           if constexpr (Lay::LINES) {
             dzq[2 * pp] = dzp[0];
@@ -816,11 +832,13 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             const float bb[4] = {bias[i].x, bias[i].y, bias[i].z, bias[i].w};
             float s[4], c[4], e[4];
             if constexpr (MODE == NT_FWD) {
+              // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi) (packed fmas); fract keeps
+              // the hardware sin/cos inside their reduced domain for any magnitude.
+              float xa[4];
+              fma4_pk(acc[i][j], xs, bias[i], xa);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                // revolutions: sin(2*pi*x) with x = omega*(z + b)/(2*pi); fract keeps the
-                // hardware sin/cos inside their reduced domain for any magnitude.
-                const float x = __builtin_amdgcn_fractf(__builtin_fmaf(acc[i][j][r], xs, bb[r]));
+                const float x = __builtin_amdgcn_fractf(xa[r]);
                 s[r] = __builtin_amdgcn_sinf(x);
                 c[r] = __builtin_amdgcn_cosf(x);
               }
@@ -843,8 +861,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             ys[h] = yh[i] = as_u2(pack4(s[0], s[1], s[2], s[3]));
             cs[h] = chh[i] = as_u2(pack4(c[0], c[1], c[2], c[3]));
             if constexpr (MODE == NT_FWD_SNAKE) es[h] = eh[i] = as_u2(pack4(e[0], e[1], e[2], e[3]));
-            if constexpr (HEAD)
-              hp[j] += s[0] * hw[i].x + s[1] * hw[i].y + s[2] * hw[i].z + s[3] * hw[i].w;
+            if constexpr (HEAD) hp[j] += dot4_pk(s, hw[i]);
           }
           if constexpr (!(Lay::LINES || Lay::HALF)) {
             yp[pp] = swap16_pair(ys[0], ys[1]);

@@ -147,6 +147,21 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const LDS_AS char*)(p);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// a[r] * s + b[r], r = 0..3, as two v_pk_fma_f32 (one correctly rounded fma per element: bit for bit
+// the four v_fma_f32 it replaces, at half their issue cost)
+__device__ __forceinline__ void fma4_pk(f32x4 a, float s, float4 b, float (&x)[4]) {
+  const f32x2 lo = __builtin_elementwise_fma(f32x2{a[0], a[1]}, f32x2{s, s}, f32x2{b.x, b.y});
+  const f32x2 hi = __builtin_elementwise_fma(f32x2{a[2], a[3]}, f32x2{s, s}, f32x2{b.z, b.w});
+  x[0] = lo.x; x[1] = lo.y; x[2] = hi.x; x[3] = hi.y;
+}
+// ((v0 w0 + v1 w1) + v2 w2) + v3 w3: the products as two v_pk_mul_f32, the sums in that order
+__device__ __forceinline__ float dot4_pk(const float (&v)[4], float4 w) {
+  const f32x2 lo = f32x2{v[0], v[1]} * f32x2{w.x, w.y};
+  const f32x2 hi = f32x2{v[2], v[3]} * f32x2{w.z, w.w};
+  return ((lo.x + lo.y) + hi.x) + hi.y;
+}
+
 __device__ __forceinline__ h16x4 pack4(float a, float b, float c, float d) {
   h16x4 r;
   r[0] = (h16)a; r[1] = (h16)b; r[2] = (h16)c; r[3] = (h16)d;

@@ -31,7 +31,7 @@ import re
 from collections import defaultdict
 
 SIMDS, XCDS, MFMA_CYC = 1024, 8, 16
-NT = re.compile(r"gemm_nt_kernel<siren::NtCfg<([^>]*)>, (\d+), (true|false)(?:, (true|false))?>")
+NT = re.compile(r"gemm_nt_kernel<siren::NtCfg<([^>]*)>, (\d+), (true|false)(?:, (true|false))?(?:, (true|false))?>")
 ONE = re.compile(r"nt_fwd_one<(\d+), (\d+)>")
 MODES = {"0": "forward (NT_FWD)", "1": "dX (NT_DX)", "2": "dX0", "7": "fused last layer (NT_FWD_HB)"}
 
@@ -72,7 +72,7 @@ def main():
             key = f"forward one wave per SIMD (pipe 5, NK {m1.group(1)}, diag {m1.group(2)})"
         else:
             key = f"{MODES.get(m.group(2), 'mode ' + m.group(2))}{' +head' if m.group(3) == 'true' else ''}" \
-                  f"{' queue' if m.group(4) == 'true' else ''}"
+                  f"{' queue' if m.group(4) == 'true' else ''}{' lines' if m.group(5) == 'true' else ''}"
         r = {"kernel": name, "dispatches": min(len(v) for v in ctrs.values())}
         gui = a.get("GRBM_GUI_ACTIVE")
         if all(c in a for c in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")):

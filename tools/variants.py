@@ -345,11 +345,17 @@ VARIANTS["ffnt"] = {"elementwise.hip": [
 VARIANTS["glds0"] = {}
 # plain (write-back) whole-line epilogue stores instead of non-temporal ones (gemm_nt.hip SIREN_NT_STNT)
 VARIANTS["stnt0"] = {}
+# the whole-line epilogue stores as volatile stores (gfx950: `sc0 sc1`, which drop the line from the
+# XCD's L2 instead of keeping it) -- do 8 MB of Y / C per tile round stop evicting W and X?
+VARIANTS["stvol"] = {"gemm_nt.hip": [(
+    "    if constexpr (SIREN_NT_STNT != 0) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (u32x4*)dst);",
+    "    if constexpr (SIREN_NT_STNT != 0) *(volatile u32x4*)dst = __builtin_bit_cast(u32x4, v);")]}
 # lines_out pairs the MFMA-layout halves into 16-B row pieces by v_permlane16_swap first (gemm_nt.hip SIREN_LINES_SWAP)
 VARIANTS["lswap"] = {}
 DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",), "stnt0": ("SIREN_NT_STNT=0",), "lswap": ("SIREN_LINES_SWAP=1",)}
 
-# tools/pending/dx_snake_lines.patch: whole-line dZ stores in the dX into a Snake layer at K <= 512
+# whole-line dZ stores in the dX into a Snake layer at K <= 512 (round 5's parked patch; adopted in the
+# product in round 6, so this patch only applies to a round-5 tree: kept as the record of the A/B)
 VARIANTS["dxsl"] = {"gemm_nt.hip": [
     ("(ACTL && MODE == NT_FWD_TANH && !HEAD));", "(ACTL && (MODE == NT_FWD_TANH || MODE == NT_DX_SNAKE) && !HEAD));"),
     ("""      auto piece = [&](auto jc, auto ppc, const uint4& cpv, const uint4& epv) {""",
