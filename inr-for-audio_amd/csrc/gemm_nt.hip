@@ -966,20 +966,23 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int i = 2 * pp + h;
-          float dz[4];
+          // (acc C) omega, paired as in the NT_DX / NT_DX0 loop below
+          f32x2 d01 = f32x2{mul_mix<0>(acc[i][j][0], cpu[h]), mul_mix<1>(acc[i][j][1], cpu[h])} * f32x2{om, om};
+          f32x2 d23 = f32x2{mul_mix<2>(acc[i][j][2], cpu[h]), mul_mix<3>(acc[i][j][3], cpu[h])} * f32x2{om, om};
+          asm volatile("" : "+v"(d01), "+v"(d23));  // rounded to fp32 before the fp16 store (fp32_first)
+          set4(cs[0][i], f32x2{cs[0][i][0], cs[0][i][1]} + d01, f32x2{cs[0][i][2], cs[0][i][3]} + d23);
+          if constexpr (nt_is_dx0(MODE)) {
+            set4(cs[1][i], __builtin_elementwise_fma(d01, f32x2{t0, t0}, f32x2{cs[1][i][0], cs[1][i][1]}),
+                 __builtin_elementwise_fma(d23, f32x2{t0, t0}, f32x2{cs[1][i][2], cs[1][i][3]}));
+            set4(cs[2][i], __builtin_elementwise_fma(d01, f32x2{t1, t1}, f32x2{cs[2][i][0], cs[2][i][1]}),
+                 __builtin_elementwise_fma(d23, f32x2{t1, t1}, f32x2{cs[2][i][2], cs[2][i][3]}));
+          }
           static_for<0, 4>([&](auto rc) {
             constexpr int r = decltype(rc)::value;
-            dz[r] = mul_mix<r>(acc[i][j][r], cpu[h]) * om;  // (acc C) omega
-            asm volatile("" : "+v"(dz[r]));  // rounded to fp32 before the fp16 store (fp32_first)
-            cs[0][i][r] += dz[r];
-            if constexpr (nt_is_dx0(MODE)) {
-              cs[1][i][r] = __builtin_fmaf(dz[r], t0, cs[1][i][r]);
-              cs[2][i][r] = __builtin_fmaf(dz[r], t1, cs[2][i][r]);
-            }
             if constexpr (MODE == NT_DX_SNAKE) cs[1][i][r] = fma_mix<r>(acc[i][j][r], epu[h], cs[1][i][r]);
             if constexpr (MODE == NT_DX0_SNAKE) cs[3][i][r] = fma_mix<r>(acc[i][j][r], epu[h], cs[3][i][r]);
           });
-          dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
+          dzp[h] = as_u2(pack4(d01.x, d01.y, d23.x, d23.y));
         }
         if constexpr (MODE == NT_DX_SNAKE && Lay::LINES) {
           dzrow[2 * pp] = dzp[0];
@@ -1048,18 +1051,19 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const int i = 2 * pp + h;
-              float dz[4];
-              static_for<0, 4>([&](auto rc) {
-                constexpr int r = decltype(rc)::value;
-                dz[r] = mul_mix<r>(acc[i][j][r], cpu[h]) * om;  // (acc C) omega
-                asm volatile("" : "+v"(dz[r]));  // rounded to fp32 before the fp16 store (fp32_first)
-                cs[0][i][r] += dz[r];
-                if constexpr (nt_is_dx0(MODE)) {
-                  cs[1][i][r] = __builtin_fmaf(dz[r], t0, cs[1][i][r]);
-                  cs[2][i][r] = __builtin_fmaf(dz[r], t1, cs[2][i][r]);
-                }
-              });
-              dzp[h] = as_u2(pack4(dz[0], dz[1], dz[2], dz[3]));
+              // (acc C) omega: the fp16 product in v_fma_mix_f32, the rest in pairs (v_pk_mul_f32,
+              // v_pk_add_f32, v_pk_fma_f32: per element the rounding of the scalar instruction)
+              f32x2 d01 = f32x2{mul_mix<0>(acc[i][j][0], cpu[h]), mul_mix<1>(acc[i][j][1], cpu[h])} * f32x2{om, om};
+              f32x2 d23 = f32x2{mul_mix<2>(acc[i][j][2], cpu[h]), mul_mix<3>(acc[i][j][3], cpu[h])} * f32x2{om, om};
+              asm volatile("" : "+v"(d01), "+v"(d23));  // rounded to fp32 before the fp16 store (fp32_first)
+              set4(cs[0][i], f32x2{cs[0][i][0], cs[0][i][1]} + d01, f32x2{cs[0][i][2], cs[0][i][3]} + d23);
+              if constexpr (nt_is_dx0(MODE)) {
+                set4(cs[1][i], __builtin_elementwise_fma(d01, f32x2{t0, t0}, f32x2{cs[1][i][0], cs[1][i][1]}),
+                     __builtin_elementwise_fma(d23, f32x2{t0, t0}, f32x2{cs[1][i][2], cs[1][i][3]}));
+                set4(cs[2][i], __builtin_elementwise_fma(d01, f32x2{t1, t1}, f32x2{cs[2][i][0], cs[2][i][1]}),
+                     __builtin_elementwise_fma(d23, f32x2{t1, t1}, f32x2{cs[2][i][2], cs[2][i][3]}));
+              }
+              dzp[h] = as_u2(pack4(d01.x, d01.y, d23.x, d23.y));
             }
             if constexpr (Lay::LINES && MODE == NT_DX) {
               dzq[2 * pp] = dzp[0];

@@ -155,6 +155,10 @@ __device__ __forceinline__ void fma4_pk(f32x4 a, float s, float4 b, float (&x)[4
   const f32x2 hi = __builtin_elementwise_fma(f32x2{a[2], a[3]}, f32x2{s, s}, f32x2{b.z, b.w});
   x[0] = lo.x; x[1] = lo.y; x[2] = hi.x; x[3] = hi.y;
 }
+// c[0..3] = the two halves
+__device__ __forceinline__ void set4(float (&c)[4], f32x2 lo, f32x2 hi) {
+  c[0] = lo.x; c[1] = lo.y; c[2] = hi.x; c[3] = hi.y;
+}
 // ((v0 w0 + v1 w1) + v2 w2) + v3 w3: the products as two v_pk_mul_f32, the sums in that order
 __device__ __forceinline__ float dot4_pk(const float (&v)[4], float4 w) {
   const f32x2 lo = f32x2{v[0], v[1]} * f32x2{w.x, w.y};

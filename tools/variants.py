@@ -345,12 +345,15 @@ VARIANTS["ffnt"] = {"elementwise.hip": [
 VARIANTS["glds0"] = {}
 # plain (write-back) whole-line epilogue stores instead of non-temporal ones (gemm_nt.hip SIREN_NT_STNT)
 VARIANTS["stnt0"] = {}
-# the whole-line epilogue stores as volatile stores (gfx950: `sc0 sc1`, which drop the line from the
-# XCD's L2 instead of keeping it) -- do 8 MB of Y / C per tile round stop evicting W and X?
-VARIANTS["stvol"] = {"gemm_nt.hip": [(
-    "    if constexpr (SIREN_NT_STNT != 0) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), (u32x4*)dst);",
-    "    if constexpr (SIREN_NT_STNT != 0) *(volatile u32x4*)dst = __builtin_bit_cast(u32x4, v);")]}
-# lines_out pairs the MFMA-layout halves into 16-B row pieces by v_permlane16_swap first (gemm_nt.hip SIREN_LINES_SWAP)
+# the whole-line epilogue stores with `sc1` (inline asm, saddr form): gfx950 drops an sc1-stored line from
+# the XCD's L2 instead of keeping it (MI355X_MICROARCH.md store table) -- do 8 MB of Y / C per tile round
+# stop evicting W and X?  (asm stores are invisible to hipcc's vmcnt counting: its waits only get stricter;
+# the s_nop covers the store-data VGPR write hazard hipcc cannot see inside asm, as _st16_asm's)
+_STSC1 = ('      stl((h16*)(ub + (size_t)(16 * q) * LD + lq), line[q]);',
+          '      { typedef unsigned u32x4 __attribute__((ext_vector_type(4)));\n'
+          '        asm volatile("global_store_dwordx4 %0, %1, %2 sc1\\n\\ts_nop 1" :: "v"(lq), "v"(__builtin_bit_cast(u32x4, line[q])),\n'
+          '                     "s"(ub + (size_t)(16 * q) * LD) : "memory"); }')
+VARIANTS["stsc1"] = {"gemm_nt.hip": [_STSC1]}
 VARIANTS["lswap"] = {}
 DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",), "stnt0": ("SIREN_NT_STNT=0",), "lswap": ("SIREN_LINES_SWAP=1",)}
 
