@@ -8,7 +8,8 @@
 #   bench_pmc_mfma.json     SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE: MFMA utilisation per kernel
 #   bench_pmc_lds.json      SQ_LDS_IDX_ACTIVE / _BANK_CONFLICT / _UNALIGNED_STALL + GRBM_GUI_ACTIVE
 #   fwd_dx_pmc_attribution.json  the forward / dX GEMMs' cycle attribution (tools/pmc_attr.py: 3 SQ / TCC passes)
-#   bench_cfg{3,4,5}.json   the other BASELINE configs' bench lines; trace_cfg{3,4,5}/ their
+#   bench_cfg{3,4,5}.json   the other BASELINE configs' bench lines (and bench_live / bench_default: the
+#                           reference's width-256 stacks, run.py:466 / run.py:30); trace_<config>/ their
 #                           rocprofv3 --kernel-trace --stats
 # Every GPU step has its own time limit and the steps are chained with &&.
 #   bash tools/profile_round.sh r02 [all|main|configs]
@@ -44,7 +45,7 @@ python3 "$ROOT/tools/trace_medians.py" "$(ls "$OUT"/trace/*kernel_trace.csv | he
 python3 "$ROOT/tools/frac_summary.py" "$OUT" || exit 2
 fi
 [ "$PART" = main ] && { echo "profile $TAG main done"; exit 0; }
-for c in cfg3 cfg4 cfg5; do
+for c in cfg3 cfg4 cfg5 live default; do
   # every config line carries its CPU baseline (cfg3 / cfg4: the SIREN port at the job's thread share)
   timeout -k 10 300 python3 "$ROOT/bench.py" --config $c > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" &&
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$c" -o run -- \

@@ -354,6 +354,63 @@ _STSC1 = ('      stl((h16*)(ub + (size_t)(16 * q) * LD + lq), line[q]);',
           '        asm volatile("global_store_dwordx4 %0, %1, %2 sc1\\n\\ts_nop 1" :: "v"(lq), "v"(__builtin_bit_cast(u32x4, line[q])),\n'
           '                     "s"(ub + (size_t)(16 * q) * LD) : "memory"); }')
 VARIANTS["stsc1"] = {"gemm_nt.hip": [_STSC1]}
+# PROBE (wrong outputs, timing only): group 0 (waves 0-3) issues every LDS-DMA and stores nothing, group 1
+# (waves 4-7) stores its own lines twice (its rows and group 0's: the same bytes) and never waits on vmcnt
+# in the K-loop -- the forward's K-loop waits then no longer sit behind the epilogue's stores in any
+# wave's in-order vmcnt.  Prices that coupling (10.8 k cycles per tile) before an LDS
+# hand-off of group 0's outputs is built.  Non-EARLY K-loop only (the plain forward).
+VARIANTS["dmag0"] = {"gemm_nt.hip": [
+    ("""    int urow[4][2];
+    unsigned pdst[4][2];""",
+     """    int urow[4][2], urowp[4][2];
+    unsigned pdst[4][2], pdstp[4][2];"""),
+    ("""        urow[pc][j] = lr0 * K * 2;
+        pdst[pc][j] = ((pc & 1) ? 0u : (unsigned)Cfg::XBYTES) + (unsigned)(lr0 * ROWB);
+      }""",
+     """        urow[pc][j] = lr0 * K * 2;
+        pdst[pc][j] = ((pc & 1) ? 0u : (unsigned)Cfg::XBYTES) + (unsigned)(lr0 * ROWB);
+        const int qr0 = (2 * (wave + 4) + j) * 8;
+        const int lq0 = (pc & 1) ? (qr0 >> 6) * 128 + (qr0 & 63) + 64 * hf : (qr0 >> 5) * 64 + (qr0 & 31) + 32 * hf;
+        urowp[pc][j] = lq0 * K * 2;
+        pdstp[pc][j] = ((pc & 1) ? 0u : (unsigned)Cfg::XBYTES) + (unsigned)(lq0 * ROWB);
+      }"""),
+    ("""        glds16x2o_asm_s(lane_src, lane_src8, (const char*)src + urow[PC][0], lds_addr(dst + pdst[PC][0]));
+      } else {""",
+     """        if (wm == 0) {
+          glds16x2o_asm_s(lane_src, lane_src8, (const char*)src + urow[PC][0], lds_addr(dst + pdst[PC][0]));
+          glds16x2o_asm_s(lane_src, lane_src8, (const char*)src + urowp[PC][0], lds_addr(dst + pdstp[PC][0]));
+        }
+      } else {"""),
+    ("""      stl((h16*)(ub + (size_t)(16 * q) * LD + lq), line[q]);
+    }
+  };""",
+     """      if (wm == 1) {
+        stl((h16*)(ub + (size_t)(16 * q) * LD + lq), line[q]);
+        stl((h16*)(ub - (size_t)256 * LD + (size_t)(16 * q) * LD + lq), line[q]);
+      }
+    }
+  };"""),
+  ],
+  "gemm_pipeline.h": [
+    ("""    if constexpr (EARLY) {
+    issue(0, 1, 1, phase_t<3>{});
+    wait_vmcnt<10>();  // K-tile 0's pieces 0..2 have landed (K0 p3, K1 p0..3 younger)
+  } else {
+    wait_vmcnt<8>();  // K-tile 0's pieces 0..2 (and the older ones) have landed
+  }""".replace("    if constexpr (EARLY) {", "  if constexpr (EARLY) {"),
+     """  if constexpr (EARLY) {
+    issue(0, 1, 1, phase_t<3>{});
+    wait_vmcnt<10>();  // K-tile 0's pieces 0..2 have landed (K0 p3, K1 p0..3 younger)
+  } else {
+    if (grp == 0) wait_vmcnt<16>();
+  }"""),
+    ("""      constexpr bool R = RELAXED || (SG == 0 && RELAXED_A);
+      wait_vmcnt<R ? 8 + E : 8>();""",
+     """      if (grp == 0) wait_vmcnt<16>();"""),
+  ]}
+# its store half alone (both groups issue their DMAs and wait as in the product): group 1 stores its lines
+# twice, group 0 none (wrong outputs, timing only) -- dmag0 minus this = the DMA / store decoupling
+VARIANTS["st1x2"] = {"gemm_nt.hip": [VARIANTS["dmag0"]["gemm_nt.hip"][3]]}
 VARIANTS["lswap"] = {}
 DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",), "stnt0": ("SIREN_NT_STNT=0",), "lswap": ("SIREN_LINES_SWAP=1",)}
 
