@@ -705,7 +705,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int i = 2 * pp + h;
-            const float4 w4 = *(const float4*)(hw_lds + nq + i * 16);
+            // the sine kind keeps phase 1's head weights in registers (same 239 VGPRs); the Snake / Tanh
+            // kinds re-read them from LDS per row (in registers they reach 255-256 VGPRs and spill)
+            const float4 w4 = (MODE == NT_FWD_HB) ? hw[i] : *(const float4*)(hw_lds + nq + i * 16);
             const uint4 pk = __builtin_bit_cast(uint4, acc[i][j]);
             const uint2 yh = uint2{pk.x, pk.y}, ch = uint2{pk.z, pk.w};
             // head_bwd_kernel's dz, ((g w) C) omega (bit-identical), times S (gm carries it; omega
