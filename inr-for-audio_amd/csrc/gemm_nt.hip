@@ -322,6 +322,48 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
   // + 3, g = lane >> 4), packed fp16: 8 B at byte 32 i + 8 g of the row's line.  Each goes into the scratch as
   // one 8-B half of its swizzled 16-B chunk 2 i + (g >> 1) (SIREN_LINES_SWAP 1: first paired into 16-B row
   // pieces across 16-lane groups by v_permlane16_swap, as round 5 did -- 4 VALU per row piece more)
+  // lines_out in two halves (the non-HALF path): lines_get exchanges one row piece through the wave's
+  // scratch into this lane's two 16-B line chunks, lines_put stores them.  The plain forward runs them
+  // a row apart, so a row's LDS round trip completes under the next row's sin / cos
+  auto lines_get = [&](const uint2 (&v)[Cfg::SN], uint4 (&line)[2]) {
+    static_assert(Cfg::SN == 4, "a wave's row piece is one 128-B line");
+    const int pr = lane & 15, pc = swap16_col(lane) >> 3;
+    const int g = lane >> 4;
+    const int qr = lane >> 3, qc = lane & 7;
+    char* sc = smem + Lay::ST + wave * 2048;
+    if constexpr (SIREN_LINES_SWAP != 0) {
+#pragma unroll
+      for (int pp = 0; pp < Cfg::SN / 2; ++pp) {
+        const int c = pp * 4 + pc;
+        *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = swap16_pair(v[2 * pp], v[2 * pp + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < Cfg::SN; ++i) {
+        const int c = 2 * i + (g >> 1);
+        *(uint2*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4) + ((g & 1) << 3)) = v[i];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // cross-lane exchange: the reads stay after every lane's writes
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = qr + 8 * q;
+      line[q] = *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4));
+    }
+    __builtin_amdgcn_wave_barrier();  // ... and the next output's writes after these reads
+  };
+  auto lines_put = [&](h16* out, int row, int col, const uint4 (&line)[2]) {
+    const int qr = lane >> 3, qc = lane & 7;
+    const char* ub = (const char*)(out + (size_t)row * LD + col);
+    unsigned lo = (unsigned)((qr * LD + qc * 8) * 2);
+    asm("" : "+v"(lo));  // kept 32-bit at the stores (a hoisted 64-bit zext defeats the saddr form)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      unsigned lq = lo;
+      asm("" : "+v"(lq));  // one opaque copy per store: no store's address is derived from another's
+      stl((h16*)(ub + (size_t)(16 * q) * LD + lq), line[q]);
+    }
+  };
   auto lines_out = [&](h16* out, int row, int col, const uint2 (&v)[Cfg::SN]) {
     static_assert(Cfg::SN == 4, "a wave's row piece is one 128-B line");
     const int pr = lane & 15, pc = swap16_col(lane) >> 3;  // this lane's piece: row, 16-B chunk
@@ -371,34 +413,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       }
       return;
     }
-    char* sc = smem + Lay::ST + wave * 2048;
-    if constexpr (SIREN_LINES_SWAP != 0) {
-#pragma unroll
-      for (int pp = 0; pp < Cfg::SN / 2; ++pp) {
-        const int c = pp * 4 + pc;
-        *(uint4*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4)) = vs[pp];
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < Cfg::SN; ++i) {
-        const int c = 2 * i + (g >> 1);
-        *(uint2*)(sc + pr * 128 + ((c ^ (pr & 7)) << 4) + ((g & 1) << 3)) = v[i];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();  // cross-lane exchange: the reads stay after every lane's writes
     uint4 line[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int r = qr + 8 * q;
-      line[q] = *(const uint4*)(sc + r * 128 + ((qc ^ (r & 7)) << 4));
-    }
-    __builtin_amdgcn_wave_barrier();  // ... and the next output's writes after these reads
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      unsigned lq = lo;
-      asm("" : "+v"(lq));  // one opaque copy per store: no store's address is derived from another's
-      stl((h16*)(ub + (size_t)(16 * q) * LD + lq), line[q]);
-    }
+    lines_get(v, line);
+    lines_put(out, row, col, line);
   };
   // NT_FWD: bias / head weights through LDS -- the epilogue then issues no global load
   // whose compiler-counted vmcnt wait would also cover the asm-issued stage prefetch.
@@ -691,6 +708,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       // Snake: row j's E pieces are loaded as phase 2 reaches row j, ahead of its dZ_L stores (the
       // registers of row j's accumulators free up as it goes); phase 3 reads them from registers
       uint4 eall[SNK ? SM : 1][SNK ? SN / 2 : 1];
+      uint4 ldz[2];  // row j-1's dZ_L line chunks
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
         if constexpr (SNK) {
@@ -738,7 +756,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
           }
           else st16((h16*)at_lane(rowp(p.dZ, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(dzp[0], dzp[1]));
         }
-        if constexpr (Lay::LINES) lines_out(p.dZ, mrowu + j * 16, n0 + wn * TN, dzq);
+        if constexpr (Lay::LINES) {
+          // a row apart, as the forward: row j-1's dZ_L stores after row j's arithmetic
+          if (j > 0) lines_put(p.dZ, mrowu + (j - 1) * 16, n0 + wn * TN, ldz);
+          lines_get(dzq, ldz);
+          if (j == SM - 1) lines_put(p.dZ, mrowu + j * 16, n0 + wn * TN, ldz);
+        }
       }
 #pragma unroll
       for (int pp = 0; pp < SN / 2; ++pp)
@@ -816,6 +839,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
       float hp[SM];
 #pragma unroll
       for (int j = 0; j < SM; ++j) hp[j] = 0.f;
+      uint4 ly[2], lc[2];  // NT_FWD: row j-1's Y / C line chunks, stored after row j's arithmetic
 #pragma unroll
       for (int j = 0; j < SM; ++j) {
         const size_t rowoff = (size_t)(mrow0 + j * 16) * LD;
@@ -876,6 +900,20 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
 #pragma unroll
           for (int i = 0; i < SN; ++i) keep ^= yh[i].x ^ yh[i].y ^ chh[i].x ^ chh[i].y;
           asm volatile("" ::"v"(keep));
+          continue;
+        }
+        if constexpr (Lay::LINES && MODE == NT_FWD && !HEAD) {
+          // a row apart: row j-1's stores after row j's arithmetic, row j's exchange now
+          if (j > 0) {
+            lines_put(p.Y, mrowu + (j - 1) * 16, n0 + wn * TN, ly);
+            lines_put(p.C, mrowu + (j - 1) * 16, n0 + wn * TN, lc);
+          }
+          lines_get(yh, ly);
+          lines_get(chh, lc);
+          if (j == SM - 1) {
+            lines_put(p.Y, mrowu + j * 16, n0 + wn * TN, ly);
+            lines_put(p.C, mrowu + j * 16, n0 + wn * TN, lc);
+          }
           continue;
         }
         if constexpr (Lay::LINES || Lay::HALF) {
@@ -1033,6 +1071,7 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         // NT_DX / NT_DX0: rows in order, both column pairs of a row together (rows >= PRE_J loaded
         // at use), then the column partials.  The same arithmetic as `piece`, kept as a plain loop:
         // written through the lambda, NT_DX0 takes 252-256 VGPRs instead of 239-244 (gfx950 listing)
+        uint4 ldz[2];  // NT_DX: row j-1's dZ line chunks
 #pragma unroll
         for (int j = 0; j < SM; ++j) {
           const size_t rowoff = (size_t)(mrow0 + j * 16) * LD;
@@ -1074,7 +1113,12 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
             else if constexpr (MODE == NT_DX)
               st16((h16*)at_lane(rowp(p.dZ, mrowu + j * 16, n0 + wn * TN), lane_piece + pp * 64), swap16_pair(dzp[0], dzp[1]));
           }
-          if constexpr (Lay::LINES && MODE == NT_DX) lines_out(p.dZ, mrowu + j * 16, n0 + wn * TN, dzq);
+          if constexpr (Lay::LINES && MODE == NT_DX) {
+            // a row apart, as the forward: row j-1's stores after row j's arithmetic
+            if (j > 0) lines_put(p.dZ, mrowu + (j - 1) * 16, n0 + wn * TN, ldz);
+            lines_get(dzq, ldz);
+            if (j == SM - 1) lines_put(p.dZ, mrowu + j * 16, n0 + wn * TN, ldz);
+          }
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
