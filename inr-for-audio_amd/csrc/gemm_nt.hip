@@ -620,6 +620,14 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         if (!(SIREN_DIAG_ON && (p.hb_fault & 1) && tn == 1))
           __hip_atomic_store(hpu + (size_t)tn * p.M + m, own == own ? __float_as_uint(own) : 0x7fc00000u,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the row's target, loaded before the partners are polled: its latency runs under the polls (loaded
+        // after them, the block waited one more memory round trip per tile)
+        // (unconditional, the row clamped into [0, n_valid), and retired unconditionally below: a load or a use
+        // under `m < n_valid` left the register's reuse in phase 2 behind a vmcnt(0), i.e. behind the dZ_L stores)
+        // (the empty asm keeps hipcc from hoisting the now always-valid load above `tid < BM`, into the waves
+        // that never consume it)
+        asm volatile("" ::: "memory");
+        const float tgt = p.target[min(m, p.n_valid > 0 ? p.n_valid - 1 : 0)];
         float o = 0.f;  // head_loss_kernel's order: partials j = 0, 1, ..., then the bias
         for (int jt = 0; jt < tiles_n; ++jt) {
           float v = own;
@@ -654,8 +662,9 @@ __global__ __launch_bounds__(Cfg::THREADS, 2) void gemm_nt_kernel(NtParams p) {
         o += hb_bias;
         const float a = p.head_omega * o;
         const float ov = p.head_omega > 0.f ? sinf(a) : o;
+        asm volatile("" ::"v"(tgt));  // consumed here on every path (the use below is under m < n_valid)
         if (m < p.n_valid) {
-          const float err = ov - p.target[m];
+          const float err = ov - tgt;
           if (p.loss_mode == 1) {
             e2 = fabsf(err);
             gv = (err > 0.f ? 1.0f : (err < 0.f ? -1.0f : 0.f)) * p.gfac;
