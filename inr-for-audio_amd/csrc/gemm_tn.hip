@@ -310,22 +310,27 @@ __global__ void dw_reduce_kernel(const float4* __restrict__ slab, int splits, in
   const int64_t total = (int64_t)ntile * TQ;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
        q += (int64_t)gridDim.x * blockDim.x) {
-    // fixed split order; the loads go out 8 at a time (a dependent load per split made the
-    // reduce latency-bound: 52 us for 128 splits of a 512^2 slab)
-    float4 v = slab[q];
-    int s = 1;
-    for (; s + 8 <= splits; s += 8) {
-      float4 w[8];
+    // fixed split order s = 0, 1, ..., splits - 1; the loads go out U at a time, the last chunk's too (a
+    // dependent load per split made the reduce latency-bound: 52 us for 128 splits of a 512^2 slab; 8 in
+    // flight and a one-at-a-time tail left width 256's 256 splits at 18 us per layer, 3.5 TB/s)
+    constexpr int U = 16;
+    float4 w[U];
+    const int n1 = splits < U ? splits : U;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) w[u] = slab[q + (int64_t)(s + u) * total];
+    for (int u = 0; u < U; ++u)
+      if (u < n1) w[u] = slab[q + (int64_t)u * total];
+    float4 v = w[0];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        v.x += w[u].x; v.y += w[u].y; v.z += w[u].z; v.w += w[u].w;
-      }
-    }
-    for (; s < splits; ++s) {
-      const float4 w = slab[q + (int64_t)s * total];
-      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    for (int u = 1; u < U; ++u)
+      if (u < n1) { v.x += w[u].x; v.y += w[u].y; v.z += w[u].z; v.w += w[u].w; }
+    for (int s = n1; s < splits; s += U) {
+      const int n = splits - s < U ? splits - s : U;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (u < n) w[u] = slab[q + (int64_t)(s + u) * total];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (u < n) { v.x += w[u].x; v.y += w[u].y; v.z += w[u].z; v.w += w[u].w; }
     }
     v.x *= inv; v.y *= inv; v.z *= inv; v.w *= inv;
     const int tile = (int)(q / TQ);
@@ -350,14 +355,15 @@ __global__ void dw_reduce_kernel(const float4* __restrict__ slab, int splits, in
 
 hipError_t dw_reduce(const float* slab, int splits, int Hin, int Hout, int tile, float* grad,
                      int accumulate, const float* gscale, hipStream_t s) {
+  // one wave per block, so that a small slab (H = 256: 16 384 float4 columns) still spreads over every CU
   const int64_t total = (int64_t)Hin * Hout / 4;
-  int grid = (int)((total + 255) / 256);
-  if (grid > 4096) grid = 4096;
+  int grid = (int)((total + 63) / 64);
+  if (grid > 8192) grid = 8192;
   if (tile == 256) {
-    hipLaunchKernelGGL(dw_reduce_kernel<TnLarge>, dim3(grid), dim3(256), 0, s, (const float4*)slab, splits,
+    hipLaunchKernelGGL(dw_reduce_kernel<TnLarge>, dim3(grid), dim3(64), 0, s, (const float4*)slab, splits,
                        Hin, Hout, grad, accumulate, gscale);
   } else if (tile == 128) {
-    hipLaunchKernelGGL(dw_reduce_kernel<TnSmall>, dim3(grid), dim3(256), 0, s, (const float4*)slab, splits,
+    hipLaunchKernelGGL(dw_reduce_kernel<TnSmall>, dim3(grid), dim3(64), 0, s, (const float4*)slab, splits,
                        Hin, Hout, grad, accumulate, gscale);
   } else {
     return hipErrorInvalidValue;
