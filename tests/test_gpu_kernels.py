@@ -342,6 +342,25 @@ def test_inner_bwd_dw(lib, dev, R, H, splits, tile, tn_pipe):
     assert np.max(np.abs(got - ref)) < 1e-5 * np.max(np.abs(ref - 0.5)) + 1e-7 * 2.0 ** -(k or 0) + 3e-8
 
 
+@pytest.mark.parametrize("H,splits,tile", [(256, 15, 256), (256, 16, 256), (256, 17, 256), (256, 256, 256),
+                                           (512, 33, 256), (256, 7, 128), (256, 40, 128)])
+def test_dw_reduce_split_order(lib, dev, H, splits, tile):
+    """The slab reduce sums the splits strictly in order s = 0, 1, ..., splits-1 in fp32 (its loads go
+    out 16 at a time, the last chunk too): checked bit for bit against numpy's sequential fp32 sum on
+    a slab whose magnitudes make the order matter.  Which slab position lands in which dW entry is
+    the kernel's MFMA-order decode, so the two are compared as sorted multisets."""
+    rng = np.random.default_rng(11)
+    n = int(lib.siren_slab_floats(H, splits)) // splits
+    slab = (rng.normal(size=(splits, n)) * 10.0 ** rng.uniform(-3, 3, size=(splits, n))).astype(F32)
+    ref = slab[0].copy()
+    for s in range(1, splits):
+        ref = (ref + slab[s]).astype(F32)
+    grad = torch.full((H, H), 7.0, device=dev)
+    ok(lib.siren_dw_reduce(ptr(to_dev(slab.reshape(-1), dev)), splits, H, tile, ptr(grad), 0, None, S()), lib)
+    got = grad.cpu().numpy().reshape(-1)
+    assert np.array_equal(np.sort(got).view(np.uint32), np.sort(ref).view(np.uint32))
+
+
 def test_col_reduce(lib, dev):
     rng = np.random.default_rng(8)
     for nrows, ncols, stride in [(3, 70, 1), (300, 256, 1), (8192, 1024, 2)]:
