@@ -412,7 +412,11 @@ VARIANTS["dmag0"] = {"gemm_nt.hip": [
 # twice, group 0 none (wrong outputs, timing only) -- dmag0 minus this = the DMA / store decoupling
 VARIANTS["st1x2"] = {"gemm_nt.hip": [VARIANTS["dmag0"]["gemm_nt.hip"][3]]}
 VARIANTS["lswap"] = {}
-DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",), "stnt0": ("SIREN_NT_STNT=0",), "lswap": ("SIREN_LINES_SWAP=1",)}
+# every ping-pong NT kernel with the EARLY tile boundary (the product takes it for the fused last layer and
+# dX0 only): round 5 measured the plain forward +2.3% at cfg2 and -2.3% at cfg4 -- a K-dependent choice?
+VARIANTS["early"] = {}
+DEFINES = {"glds0": ("SIREN_GLDS_PAIR=0",), "stnt0": ("SIREN_NT_STNT=0",), "lswap": ("SIREN_LINES_SWAP=1",),
+           "early": ("SIREN_NT_EARLY=1",)}
 
 # whole-line dZ stores in the dX into a Snake layer at K <= 512 (round 5's parked patch; adopted in the
 # product in round 6, so this patch only applies to a round-5 tree: kept as the record of the A/B)
